@@ -1,0 +1,182 @@
+/*
+ * mcmc_hip.h -- C ABI of the MI355X (gfx950) many-chain MCMC inner loop.
+ *
+ * Drop-in boundary for MCMC.jl's model x sampler x runner hot path
+ * (reference: /root/reference, Julia 0.2).  Plain C types only: int32/int64,
+ * double*, uint64_t*; no torch, no C++ in the signatures.  A Julia host binds
+ * these with `ccall` (INTEGRATION.md shows the binding); the in-tree host is
+ * Python/ctypes (mcmc.jl_amd/mcmchip).
+ *
+ *   reference interface                              replaced by
+ *   -----------------------------------------------  -------------------------------------------
+ *   model(f; init, grad, scale)      mcmcmodels.jl:27-33,   mcmc_model_create (catalogue kind, init,
+ *     MCMCLikelihoodModel ctor        likmodel.jl:100-143    scale, data X/Y)
+ *   RWM / MALA / HMC / HMCDA ctors   RWM.jl:24-36,          mcmc_sampler_cfg (validated like the
+ *                                    MALA.jl:50-62,         reference @asserts: mcmc_sampler_validate)
+ *                                    HMC.jl:53-74,
+ *                                    HMCDA.jl:24-43
+ *   EmpMCTuner                       samplers.jl:32-50      mcmc_sampler_cfg.tuner_*
+ *   SerialMC(steps,burnin,thinning)  SerialMC.jl:12-35      mcmc_runner_cfg
+ *   m * s * r -> MCMCTask (spinTask) MCMC.jl:87-98,         mcmc_chains_create (a batch of C
+ *                                    samplers.jl:53          independent MCMCTasks: one per chain)
+ *   run(t::MCMCTask) / run_serialmc  runners.jl:7-11,45,    mcmc_run_serialmc
+ *                                    SerialMC.jl:37-85
+ *   run(c::MCMCChain) (continue)     runners.jl:14          mcmc_run_serialmc again on the same chains
+ *   resume(c; steps)                 SerialMC.jl:93-97      mcmc_chains_reset + mcmc_run_serialmc
+ *   MCMCChain fields                 MCMC.jl:58-80          mcmc_outputs (samples, gradients,
+ *                                                           accept bits, runtime)
+ *   acceptance(chain)                summary.jl:6-15        computed by the host from accept bits
+ *
+ * Errors: every call returns an int status (MCMC_OK = 0) and sets a
+ * thread-local message readable with mcmc_last_error(); the reference's
+ * @assert texts are reproduced verbatim where one exists.
+ *
+ * Threading: one host thread drives a context; calls on one context are not
+ * re-entrant; distinct contexts are independent.  Ownership: the caller owns
+ * every output buffer; the library owns device state inside ctx/model/chains
+ * and never keeps a caller pointer after a call returns.
+ */
+#ifndef MCMC_HIP_H
+#define MCMC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCMC_ABI_VERSION 1
+
+/* status codes */
+enum {
+    MCMC_OK = 0,
+    MCMC_E_INVALID_ARG = 1,          /* a reference @assert failed, or a NULL/size error            */
+    MCMC_E_INIT_OUT_OF_SUPPORT = 2,  /* "Initial values out of model support, try other values"    */
+    MCMC_E_NEEDS_GRADIENT = 3,       /* "<S> sampler requires model with gradient function"         */
+    MCMC_E_HIP = 4,                  /* a HIP runtime call failed                                   */
+    MCMC_E_OOM = 5,                  /* device allocation failed                                    */
+    MCMC_E_UNSUPPORTED = 6           /* model x sampler x size combination not built                */
+};
+
+/* model catalogue (Julia closures cannot cross a C ABI) */
+enum {
+    MCMC_MODEL_ISO_NORMAL_DOT = 1,   /* model(v -> -dot(v,v), grad = v -> -2v)   README.md:60,63      */
+    MCMC_MODEL_NORMAL_DSL = 2,       /* model(:(v ~ Normal(mu, sigma)), gradient=true)  README.md:67-72 */
+    MCMC_MODEL_LOGISTIC = 3,         /* examples/logistic_regression.jl:16-22 (DSL, gradient=true)   */
+    MCMC_MODEL_LINEAR = 4            /* examples/linear_regression.jl:14-20  (DSL, gradient=true)    */
+};
+
+/* samplers */
+enum { MCMC_RWM = 1, MCMC_MALA = 2, MCMC_HMC = 3, MCMC_HMCDA = 4 };
+
+typedef struct mcmc_ctx mcmc_ctx;
+typedef struct mcmc_model mcmc_model;
+typedef struct mcmc_chains mcmc_chains;
+
+typedef struct {
+    int32_t kind;            /* MCMC_MODEL_*                                                     */
+    int32_t has_gradient;    /* 0: eval only (hasgradient(model) == false, mcmcmodels.jl:19)      */
+    int64_t d;               /* parameter vector size (model.size)                               */
+    const double* init;      /* [d]  model.init                                                  */
+    const double* scale;     /* [d]  model.scale (NULL -> ones)                                   */
+    double mu, sigma;        /* NORMAL_DSL: Normal(mu, sigma)                                     */
+    double prior_sigma;      /* LOGISTIC/LINEAR: vars ~ Normal(0, prior_sigma)                    */
+    double noise_sigma;      /* LINEAR: resid ~ Normal(0, noise_sigma)                             */
+    double link_sign;        /* LOGISTIC: +1 -> prob = 1/(1+exp(-X*vars)) (example),
+                                          -1 -> prob = 1/(1+exp(+X*vars)) (test/test_syntax.jl:13) */
+    int64_t n;               /* observations                                                      */
+    const double* X;         /* [n][d] row-major covariates                                        */
+    const double* Y;         /* [n] responses (LOGISTIC: 0.0 / 1.0)                                */
+} mcmc_model_desc;
+
+typedef struct {
+    int32_t kind;            /* MCMC_RWM | MCMC_MALA | MCMC_HMC | MCMC_HMCDA                      */
+    double scale;            /* RWM: scale (RWM.jl:25)                                             */
+    double drift_step;       /* MALA: driftStep (MALA.jl:51)                                       */
+    int64_t n_leaps;         /* HMC: nLeaps (HMC.jl:54)                                            */
+    double leap_step;        /* HMC: leapStep (HMC.jl:55)                                          */
+    double rate, len, shrinkage, t0, step;   /* HMCDA (HMCDA.jl:25-29)                             */
+    int32_t tuner;           /* 0: nothing; 1: EmpiricalMCMCTuner (MALA, HMC)                      */
+    int64_t adapt_step, max_step;            /* EmpMCTuner (samplers.jl:33-37)                      */
+    double target_path, target_rate;
+    int64_t max_leaps;       /* HMCDA/HMC-tuner safety cap on leapfrogs per step (0 -> 1<<20)      */
+} mcmc_sampler_cfg;
+
+typedef struct {
+    int64_t burnin;          /* SerialMC.burnin                                                    */
+    int64_t thinning;        /* SerialMC.thinning                                                  */
+    int64_t len;             /* SerialMC.len: steps consumed per run                              */
+} mcmc_runner_cfg;
+
+/* Output buffers.  Any pointer may be NULL (not wanted).  Layouts:
+ *   samples, gradients : [nkept][d][nchains]   (MCMCChain.samples / .gradients, per chain c:
+ *                                              samples[j][:, c] is row j of its DataFrame)
+ *   accept_bits        : [nkept][ceil(nchains/64)]  bit (c % 64) of word c/64 = diagnostics["accept"][j]
+ *   final_x            : [d][nchains]          state after the run
+ *   final_lp           : [nchains]
+ * nkept = length((burnin+1):thinning:len).  on_device != 0 means every pointer is a
+ * device pointer on the context's GPU (e.g. torch tensors): nothing crosses PCIe. */
+typedef struct {
+    double* samples;
+    double* gradients;
+    uint64_t* accept_bits;
+    double* final_x;
+    double* final_lp;
+    int32_t on_device;
+    double runtime_s;        /* out: wall time of the step loop (MCMCChain.runTime, SerialMC.jl:38,84) */
+    double kernel_ms;        /* out: device time of the step kernels (HIP events)                     */
+    int64_t nkept;           /* out */
+} mcmc_outputs;
+
+/* ---- library ---- */
+const char* mcmc_last_error(void);
+int mcmc_abi_version(void);
+int mcmc_device_count(int* count);
+
+/* ---- context: one GPU, one stream ---- */
+int mcmc_ctx_create(int device, mcmc_ctx** out);
+int mcmc_ctx_destroy(mcmc_ctx* ctx);
+int mcmc_ctx_synchronize(mcmc_ctx* ctx);
+
+/* ---- model: uploads init/scale/X/Y once (model data is replicated per GPU) ---- */
+int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcmc_model** out);
+int mcmc_model_destroy(mcmc_model* model);
+/* evaluate log-target (and gradient) of `nchains` parameter vectors x[d][nchains] on the device
+ * (model.eval / model.evalallg, likmodel.jl:21,25); host pointers. grad may be NULL. */
+int mcmc_model_eval(mcmc_model* model, int64_t nchains, const double* x, double* lp, double* grad);
+
+/* ---- sampler config validation (the reference constructors' @asserts) ---- */
+int mcmc_sampler_validate(const mcmc_sampler_cfg* cfg);
+int mcmc_runner_validate(const mcmc_runner_cfg* cfg);
+
+/* ---- chains: C independent MCMCTasks of one (model, sampler) on one GPU ----
+ * chain_offset = global id of local chain 0 (multi-GPU sharding): the random
+ * stream is keyed by (seed, global chain, global step), so results do not
+ * depend on the number of GPUs.  init_x: optional per-chain start [d][nchains]
+ * (NULL -> every chain starts at model.init, RWM.jl:53). */
+int mcmc_chains_create(mcmc_model* model, const mcmc_sampler_cfg* sampler, int64_t nchains,
+                       int64_t chain_offset, uint64_t seed, const double* init_x, mcmc_chains** out);
+int mcmc_chains_destroy(mcmc_chains* chains);
+/* restart from model.init (resume(), SerialMC.jl:93-97): step counter back to 0. */
+int mcmc_chains_reset(mcmc_chains* chains);
+/* steps consumed so far (the sampler's own loop counter i). */
+int mcmc_chains_steps_done(mcmc_chains* chains, int64_t* steps);
+/* steps fused per kernel launch (0 = whole run in one launch, the default). */
+int mcmc_chains_set_steps_per_launch(mcmc_chains* chains, int64_t steps_per_launch);
+/* store gradients of kept samples for gradient samplers (default 1, SerialMC.jl:51-53) */
+int mcmc_chains_set_store_gradients(mcmc_chains* chains, int32_t store);
+
+/* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
+int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);
+
+/* ---- diagnostics used by the parity tests: evaluate the build's deterministic
+ *      math on the device.  op: 0 log, 1 exp, 2 sin2pi, 3 cos2pi,
+ *      4 sqrt, 5 div(x, y), 6 normals (x = block counters). ---- */
+int mcmc_debug_detmath(mcmc_ctx* ctx, int op, int64_t n, const double* x, const double* y, double* out);
+int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr /*[n][4]*/, const uint32_t* key /*[n][2]*/,
+                      uint32_t* out /*[n][4]*/);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,186 @@
+// detmath.hpp -- device-side random stream and deterministic fp64 math for gfx950.
+//
+// Specification: DESIGN.md §3.  Every function here has a CPU twin in
+// oracle/detmath.h that performs the same IEEE operations in the same order,
+// so kernel and oracle agree bit for bit.  Rules that make that hold:
+//   * the whole library is compiled with -ffp-contract=off; each fused
+//     multiply-add is an explicit __builtin_fma;
+//   * '/' and sqrt are the IEEE correctly-rounded operations (hipcc's default
+//     f64 lowering; checked on the device by tests/test_gpu_detmath.py);
+//   * no OCML transcendentals (their last-ulp behaviour differs from glibc).
+//
+// The reference draws with Julia's global dSFMT + ziggurat (src/samplers/RWM.jl:59,
+// src/samplers/HMC.jl:136); the build replaces that with a counter-based
+// Philox4x32-10 stream keyed by the run seed, counter = (global chain, step,
+// block, tag), so every (chain, step) draw is addressable without state and the
+// result does not depend on how chains are sharded over GPUs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mcmc {
+
+enum : uint32_t { TAG_NORMAL = 0u, TAG_ACCEPT = 1u, TAG_DATA = 7u };
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                               uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+    }
+    return {c0, c1, c2, c3};
+}
+
+struct Stream {
+    uint32_t k0, k1;
+    __device__ __forceinline__ u32x4 block(uint32_t chain, uint32_t step, uint32_t blk, uint32_t tag) const {
+        return philox4x32_10(chain, step, blk, tag, k0, k1);
+    }
+};
+
+__device__ __forceinline__ double bits2d(uint64_t b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ uint64_t d2bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+__device__ __forceinline__ double uniform53(uint32_t a, uint32_t b) {
+    const uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return (double)m * 0x1p-53;
+}
+__device__ __forceinline__ double uniform32_open(uint32_t a) { return ((double)a + 0.5) * 0x1p-32; }
+__device__ __forceinline__ double uniform32(uint32_t a) { return (double)a * 0x1p-32; }
+__device__ __forceinline__ double pow2i(int k) { return bits2d((uint64_t)(k + 1023) << 52); }
+
+// fdlibm e_log.c general path.  Special cases resolved by selects so the
+// common path stays branch-free across the wave.
+__device__ __forceinline__ double det_log(double x) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2,
+                 Lg3 = 0x1.2492494229359p-2, Lg4 = 0x1.c71c51d8e78afp-3,
+                 Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    uint64_t bx = d2bits(x);
+    int k = 0;
+    const bool sub = bx < 0x0010000000000000ull;            // zero or subnormal (or negative: handled below)
+    if (sub && x > 0.0) { x = x * 0x1p54; k = -54; bx = d2bits(x); }
+    uint32_t hx = (uint32_t)(bx >> 32);
+    k += (int)((hx >> 20) & 0x7ff) - 1023;
+    hx &= 0x000fffffu;
+    const uint32_t i = (hx + 0x95f64u) & 0x100000u;
+    const uint64_t nb = ((uint64_t)(hx | (i ^ 0x3ff00000u)) << 32) | (bx & 0xffffffffull);
+    const double m = bits2d(nb);
+    k += (int)(i >> 20);
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double dk = (double)k;
+    const double z = s * s;
+    const double w = z * z;
+    const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
+    const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    double res = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    // special values, in the oracle's order: NaN, negative, zero, +inf
+    if (x == 0.0) res = -__builtin_inf();
+    if (bx >= 0x7ff0000000000000ull && x > 0.0) res = x;     // +inf
+    if (x < 0.0) res = bits2d(0x7ff8000000000000ull);
+    if (x != x) res = x;
+    return res;
+}
+
+__device__ __forceinline__ double det_exp(double x) {
+    const double inv_ln2 = 0x1.71547652b82fep+0;
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double shifter = 0x1.8p52;
+    const double xc = __builtin_fmin(__builtin_fmax(x, -746.0), 710.0);  // keep k in range for NaN-free math
+    const double t = __builtin_fma(xc, inv_ln2, shifter);
+    const double kd = t - shifter;
+    const int k = (int)kd;
+    double r = __builtin_fma(-kd, ln2_hi, xc);
+    r = __builtin_fma(-kd, ln2_lo, r);
+    double p = 0x1.6124613a86d09p-33;
+    p = __builtin_fma(p, r, 0x1.1eed8eff8d898p-29);
+    p = __builtin_fma(p, r, 0x1.ae64567f544e4p-26);
+    p = __builtin_fma(p, r, 0x1.27e4fb7789f5cp-22);
+    p = __builtin_fma(p, r, 0x1.71de3a556c734p-19);
+    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-16);
+    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-13);
+    p = __builtin_fma(p, r, 0x1.6c16c16c16c17p-10);
+    p = __builtin_fma(p, r, 0x1.1111111111111p-7);
+    p = __builtin_fma(p, r, 0x1.5555555555555p-5);
+    p = __builtin_fma(p, r, 0x1.5555555555555p-3);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    const int k1 = k / 2, k2 = k - k1;
+    double res = (p * pow2i(k1)) * pow2i(k2);
+    if (x > 709.782712893384) res = __builtin_inf();
+    if (x < -745.1332191019412) res = 0.0;
+    if (x != x) res = x;
+    return res;
+}
+
+__device__ __forceinline__ void det_sincos2pi(double u, double& s_out, double& c_out) {
+    const double q = __builtin_floor(__builtin_fma(u, 4.0, 0.5));
+    const double r = __builtin_fma(q, -0.25, u);
+    const double r2 = r * r;
+    double S = -0x1.6fadb9f155744p-1;
+    S = __builtin_fma(S, r2, 0x1.e8f434d018d63p+1);
+    S = __builtin_fma(S, r2, -0x1.e3074fde8871fp+3);
+    S = __builtin_fma(S, r2, 0x1.50783487ee782p+5);
+    S = __builtin_fma(S, r2, -0x1.32d2cce62bd86p+6);
+    S = __builtin_fma(S, r2, 0x1.466bc6775aae2p+6);
+    S = __builtin_fma(S, r2, -0x1.4abbce625be53p+5);
+    S = __builtin_fma(S, r2, 0x1.921fb54442d18p+2);
+    double C = 0x1.20c62c2f2d7f5p-2;
+    C = __builtin_fma(C, r2, -0x1.b6e24f44b128fp+0);
+    C = __builtin_fma(C, r2, 0x1.f9d38a3763cc3p+2);
+    C = __builtin_fma(C, r2, -0x1.a6d1f2a204a8cp+4);
+    C = __builtin_fma(C, r2, 0x1.e1f506891babbp+5);
+    C = __builtin_fma(C, r2, -0x1.55d3c7e3cbffap+6);
+    C = __builtin_fma(C, r2, 0x1.03c1f081b5ac4p+6);
+    C = __builtin_fma(C, r2, -0x1.3bd3cc9be45dep+4);
+    C = __builtin_fma(C, r2, 1.0);
+    const double sn = r * S;
+    const int qi = ((int)q) & 3;
+    const double a = (qi & 1) ? C : sn;    // |sin| part
+    const double b = (qi & 1) ? sn : C;    // |cos| part
+    s_out = (qi & 2) ? -a : a;
+    c_out = (qi == 1 || qi == 2) ? -b : b;
+}
+
+// Two Box-Muller pairs from one Philox block.
+__device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3) {
+    {
+        const double rad = __builtin_sqrt(-2.0 * det_log(uniform32_open(w.x)));
+        double s, c;
+        det_sincos2pi(uniform32(w.y), s, c);
+        z0 = rad * c; z1 = rad * s;
+    }
+    {
+        const double rad = __builtin_sqrt(-2.0 * det_log(uniform32_open(w.z)));
+        double s, c;
+        det_sincos2pi(uniform32(w.w), s, c);
+        z2 = rad * c; z3 = rad * s;
+    }
+}
+
+__device__ __forceinline__ double round_away(double x) {
+    double t = __builtin_trunc(x);
+    const double fr = x - t;
+    if (fr >= 0.5) t += 1.0;
+    else if (fr <= -0.5) t -= 1.0;
+    return t;
+}
+
+}  // namespace mcmc

@@ -1,0 +1,674 @@
+// runtime.cpp -- host runtime behind the C ABI (include/mcmc_hip.h).
+//
+// Owns device contexts, model uploads, per-chain state and the SerialMC step
+// loop.  Everything numeric runs in the HIP kernels; the host validates
+// arguments (the reference's @asserts), plans launches and moves buffers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/mcmc_hip.h"
+#include "../common.hpp"
+#include "kernels_api.hpp"
+
+using namespace mcmc;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            return fail(e_ == hipErrorOutOfMemory ? MCMC_E_OOM : MCMC_E_HIP,                   \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                    \
+        }                                                                                      \
+    } while (0)
+
+extern "C" const char* mcmc_last_error(void) { return g_err.c_str(); }
+extern "C" int mcmc_abi_version(void) { return MCMC_ABI_VERSION; }
+extern "C" int mcmc_device_count(int* count) {
+    if (!count) return fail(MCMC_E_INVALID_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return MCMC_OK;
+}
+
+// ------------------------------------------------------------------ objects
+struct mcmc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int32_t* d_err = nullptr;
+};
+
+struct mcmc_model {
+    mcmc_ctx* ctx = nullptr;
+    ModelArgs args{};
+    int has_gradient = 0;
+    std::vector<double> init, scale;
+    double* d_init = nullptr;
+    double* d_scale = nullptr;
+    double* d_X = nullptr;
+    double* d_Y = nullptr;
+};
+
+enum Layout { LAYOUT_LPC = 0, LAYOUT_WPC = 1 };
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct mcmc_chains {
+    mcmc_model* model = nullptr;
+    SamplerArgs sa{};
+    int64_t C = 0, ld = 0, offset = 0;
+    uint64_t seed = 0;
+    Layout layout = LAYOUT_LPC;
+    ChainState st{};
+    double* d_scale_eff = nullptr;   // model.scale .* sampler.scale (RWM.jl:52)
+    double* d_init_x = nullptr;      // optional per-chain start, state layout
+    int64_t steps_done = 0;
+    int64_t spl = 0;                 // steps per launch (0: whole run)
+    int store_grads = 1;
+    DevBuf out_samples, out_grads, out_bits, out_tmp;
+};
+
+static int set_device(mcmc_ctx* ctx) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    return MCMC_OK;
+}
+
+template <class T>
+static int dmalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return MCMC_OK;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail(MCMC_E_OOM, std::string("hipMalloc(") + std::to_string(count * sizeof(T)) + " B): " +
+                                    hipGetErrorString(e));
+    }
+    return MCMC_OK;
+}
+
+static void dfree(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+static int ensure(DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return MCMC_OK;
+    dfree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    if (bytes == 0) return MCMC_OK;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(MCMC_E_OOM, std::string("hipMalloc(") + std::to_string(bytes) + " B) for outputs: " +
+                                    hipGetErrorString(e));
+    }
+    b.bytes = bytes;
+    return MCMC_OK;
+}
+
+// ------------------------------------------------------------------ context
+extern "C" int mcmc_ctx_create(int device, mcmc_ctx** out) {
+    if (!out) return fail(MCMC_E_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(MCMC_E_HIP, "no HIP device available");
+    if (device < 0 || device >= n) return fail(MCMC_E_INVALID_ARG, "device ordinal out of range");
+    auto* c = new mcmc_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_err, sizeof(int32_t));
+    if (e != hipSuccess) {
+        delete c;
+        return fail(MCMC_E_HIP, std::string("context creation: ") + hipGetErrorString(e));
+    }
+    *out = c;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_ctx_destroy(mcmc_ctx* ctx) {
+    if (!ctx) return MCMC_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    dfree(ctx->d_err);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_ctx_synchronize(mcmc_ctx* ctx) {
+    if (!ctx) return fail(MCMC_E_INVALID_ARG, "ctx is NULL");
+    if (int r = set_device(ctx)) return r;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MCMC_OK;
+}
+
+// ------------------------------------------------------------------ validation
+
+extern "C" int mcmc_sampler_validate(const mcmc_sampler_cfg* s) {
+    if (!s) return fail(MCMC_E_INVALID_ARG, "sampler cfg is NULL");
+    switch (s->kind) {
+        case MCMC_RWM:
+            if (!(s->scale > 0)) return fail(MCMC_E_INVALID_ARG, "scale should be > 0");               // RWM.jl:29
+            if (s->tuner) return fail(MCMC_E_UNSUPPORTED, "RWM has no tuner in the reference (RWMTuner is abstract)");
+            break;
+        case MCMC_MALA:
+            if (!(s->drift_step > 0)) return fail(MCMC_E_INVALID_ARG, "MALA drift step should be > 0"); // MALA.jl:55
+            break;
+        case MCMC_HMC:
+            if (!(s->n_leaps > 0)) return fail(MCMC_E_INVALID_ARG, "inner steps should be > 0");        // HMC.jl:60
+            if (!(s->leap_step > 0)) return fail(MCMC_E_INVALID_ARG, "inner steps scaling should be > 0"); // HMC.jl:61
+            break;
+        case MCMC_HMCDA: {
+            char buf[160];
+            if (!(0.0 < s->rate && s->rate < 1.0)) {
+                snprintf(buf, sizeof buf, "Target acceptance rate (%g) should be between 0 and 1", s->rate);
+                return fail(MCMC_E_INVALID_ARG, buf);                                                    // HMCDA.jl:33
+            }
+            if (!(s->len > 0)) {
+                snprintf(buf, sizeof buf, "len parameter of HMCDA sampler (%g) must be non-negative", s->len);
+                return fail(MCMC_E_INVALID_ARG, buf);                                                    // HMCDA.jl:34
+            }
+            if (!(s->shrinkage > 0)) {
+                snprintf(buf, sizeof buf, "shrinkage parameter of HMCDA sampler (%g) must be positive", s->shrinkage);
+                return fail(MCMC_E_INVALID_ARG, buf);                                                    // HMCDA.jl:35
+            }
+            if (!(s->t0 >= 0)) {
+                snprintf(buf, sizeof buf, "t0 parameter of HMCDA sampler (%g) must be non-negative", s->t0);
+                return fail(MCMC_E_INVALID_ARG, buf);                                                    // HMCDA.jl:36
+            }
+            if (s->tuner) return fail(MCMC_E_UNSUPPORTED, "HMCDA takes no tuner");
+            break;
+        }
+        default:
+            return fail(MCMC_E_UNSUPPORTED, "unknown sampler kind");
+    }
+    if (s->tuner) {
+        char buf[160];
+        if (!(s->adapt_step > 0)) {
+            snprintf(buf, sizeof buf, "Adaptation step size (%lld) should be > 0", (long long)s->adapt_step);
+            return fail(MCMC_E_INVALID_ARG, buf);                                                        // samplers.jl:40
+        }
+        if (!(s->max_step > 0)) {
+            snprintf(buf, sizeof buf, "Adaptation step size (%lld) should be > 0", (long long)s->max_step);
+            return fail(MCMC_E_INVALID_ARG, buf);                                                        // samplers.jl:41
+        }
+        if (!(0.0 < s->target_rate && s->target_rate < 1.0)) {
+            snprintf(buf, sizeof buf, "Target acceptance rate (%g) should be between 0 and 1", s->target_rate);
+            return fail(MCMC_E_INVALID_ARG, buf);                                                        // samplers.jl:42
+        }
+    }
+    if (s->max_leaps < 0) return fail(MCMC_E_INVALID_ARG, "max_leaps should be >= 0");
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_runner_validate(const mcmc_runner_cfg* r) {
+    if (!r) return fail(MCMC_E_INVALID_ARG, "runner cfg is NULL");
+    char buf[160];
+    if (!(r->burnin >= 0)) {
+        snprintf(buf, sizeof buf, "Burnin rounds (%lld) should be >= 0", (long long)r->burnin);
+        return fail(MCMC_E_INVALID_ARG, buf);                                                            // SerialMC.jl:25
+    }
+    if (!(r->len > r->burnin)) {
+        snprintf(buf, sizeof buf, "Total MCMC length (%lld) should be > to burnin (%lld)", (long long)r->len,
+                 (long long)r->burnin);
+        return fail(MCMC_E_INVALID_ARG, buf);                                                            // SerialMC.jl:26
+    }
+    if (!(r->thinning >= 1)) {
+        snprintf(buf, sizeof buf, "Thinning (%lld) should be >= 1", (long long)r->thinning);
+        return fail(MCMC_E_INVALID_ARG, buf);                                                            // SerialMC.jl:27
+    }
+    if (r->len > 0x7fffffffLL) return fail(MCMC_E_INVALID_ARG, "len exceeds the 2^31 step counter");
+    return MCMC_OK;
+}
+
+static int64_t nkept_of(const mcmc_runner_cfg& r) {
+    if (r.len <= r.burnin) return 0;
+    return (r.len - r.burnin - 1) / r.thinning + 1;
+}
+
+// ------------------------------------------------------------------ model
+extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcmc_model** out) {
+    if (!ctx || !desc || !out) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (int r = set_device(ctx)) return r;
+    const int64_t d = desc->d;
+    if (d <= 0) return fail(MCMC_E_INVALID_ARG, "model size d should be > 0");
+    if (!desc->init) return fail(MCMC_E_INVALID_ARG, "model init is NULL");
+    auto* m = new mcmc_model();
+    m->ctx = ctx;
+    m->init.assign(desc->init, desc->init + d);
+    m->scale.assign((size_t)d, 1.0);
+    if (desc->scale) m->scale.assign(desc->scale, desc->scale + d);
+    m->has_gradient = desc->has_gradient;
+    ModelArgs& a = m->args;
+    a.kind = desc->kind;
+    a.d = (int32_t)d;
+    a.mu = desc->mu;
+    a.sigma = desc->sigma;
+    a.prior_sigma = desc->prior_sigma;
+    a.noise_sigma = desc->noise_sigma;
+    a.link_sign = desc->link_sign;
+    a.n = 0;
+    a.n_pad = 0;
+    auto bail = [&](int code) {
+        mcmc_model_destroy(m);
+        return code;
+    };
+    switch (desc->kind) {
+        case MCMC_MODEL_ISO_NORMAL_DOT:
+            break;
+        case MCMC_MODEL_NORMAL_DSL:
+            if (!(desc->sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "Normal sigma should be > 0"));
+            break;
+        case MCMC_MODEL_LOGISTIC:
+        case MCMC_MODEL_LINEAR:
+            return bail(fail(MCMC_E_UNSUPPORTED, "regression models are not built in this library version"));
+        default:
+            return bail(fail(MCMC_E_UNSUPPORTED, "unknown model kind"));
+    }
+    if (d > 0x7fffffff) return bail(fail(MCMC_E_INVALID_ARG, "d too large"));
+    if (int r = dmalloc(&m->d_init, (size_t)d)) return bail(r);
+    if (int r = dmalloc(&m->d_scale, (size_t)d)) return bail(r);
+    a.init = m->d_init;
+    hipError_t e = hipMemcpy(m->d_init, m->init.data(), (size_t)d * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(m->d_scale, m->scale.data(), (size_t)d * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return bail(fail(MCMC_E_HIP, std::string("model upload: ") + hipGetErrorString(e)));
+    // likmodel.jl:54  @assert isfinite(f(i)) "Initial values out of model support, try other values"
+    double lp = 0;
+    if (int r = mcmc_model_eval(m, 1, m->init.data(), &lp, nullptr)) return bail(r);
+    if (!std::isfinite(lp))
+        return bail(fail(MCMC_E_INIT_OUT_OF_SUPPORT, "Initial values out of model support, try other values"));
+    *out = m;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_model_destroy(mcmc_model* m) {
+    if (!m) return MCMC_OK;
+    (void)hipSetDevice(m->ctx->device);
+    dfree(m->d_init);
+    dfree(m->d_scale);
+    dfree(m->d_X);
+    dfree(m->d_Y);
+    delete m;
+    return MCMC_OK;
+}
+
+static bool model_is_separable(const mcmc_model* m) {
+    return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL;
+}
+
+static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+static LpcArgs base_args(const mcmc_model* m, int64_t C, int64_t ld) {
+    LpcArgs a{};
+    a.m = m->args;
+    a.s.C = C;
+    a.s.ld = ld;
+    a.s.d = m->args.d;
+    a.s.err = m->ctx->d_err;
+    a.s.thinning = 1;
+    return a;
+}
+
+extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, double* lp, double* grad) {
+    if (!m || !x || !lp) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    if (nchains <= 0) return fail(MCMC_E_INVALID_ARG, "nchains should be > 0");
+    mcmc_ctx* ctx = m->ctx;
+    if (int r = set_device(ctx)) return r;
+    const int d = m->args.d;
+    if (!model_is_separable(m)) return fail(MCMC_E_UNSUPPORTED, "model kind has no eval kernel");
+    if (d > mcmc_lpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "eval for d > 32 is served by the wave-per-chain path");
+    double *dx = nullptr, *dlp = nullptr, *dg = nullptr;
+    int rc = MCMC_OK;
+    do {
+        if ((rc = dmalloc(&dx, (size_t)d * nchains))) break;
+        if ((rc = dmalloc(&dlp, (size_t)nchains))) break;
+        if (grad && (rc = dmalloc(&dg, (size_t)d * nchains))) break;
+        hipError_t e = hipMemcpy(dx, x, (size_t)d * nchains * 8, hipMemcpyHostToDevice);
+        LpcArgs a = base_args(m, nchains, nchains);
+        if (e == hipSuccess) e = mcmc_launch_lpc_eval(a, dx, nchains, dlp, dg, 0, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = hipMemcpy(lp, dlp, (size_t)nchains * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && grad) e = hipMemcpy(grad, dg, (size_t)d * nchains * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("model eval: ") + hipGetErrorString(e));
+    } while (0);
+    dfree(dx);
+    dfree(dlp);
+    dfree(dg);
+    return rc;
+}
+
+// ------------------------------------------------------------------ chains
+static void free_state(mcmc_chains* c) {
+    ChainState& s = c->st;
+    dfree(s.x); dfree(s.lp); dfree(s.g); dfree(s.t_step); dfree(s.t_bar); dfree(s.t_h);
+    dfree(s.t_leaps); dfree(s.t_acc); dfree(s.t_prop);
+    s = ChainState{};
+}
+
+// Put every chain at its start and reset the sampler's state (SamplerTask initialisation).
+static int init_state(mcmc_chains* c) {
+    mcmc_model* m = c->model;
+    mcmc_ctx* ctx = m->ctx;
+    const int d = m->args.d;
+    const SamplerArgs& sa = c->sa;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int32_t), st));
+    if (c->d_init_x) HIP_TRY(mcmc_copy_cols(c->st.x, c->ld, c->d_init_x, c->ld, d, c->C, st));
+    else HIP_TRY(mcmc_broadcast_cols(c->st.x, c->ld, m->d_init, d, c->C, st));
+    LpcArgs a = base_args(m, c->C, c->ld);
+    HIP_TRY(mcmc_launch_lpc_eval(a, c->st.x, c->ld, c->st.lp, nullptr, 1, st));
+    if (sa.kind == SK_MALA && sa.tuner) HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, sa.drift_step, st));
+    if (sa.kind == SK_HMC && sa.tuner) {
+        HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, sa.leap_step, st));
+        HIP_TRY(mcmc_fill_i32(c->st.t_leaps, c->C, (int32_t)sa.n_leaps, st));
+    }
+    if (sa.kind == SK_HMCDA) {
+        // initializeHMCDAStep returns 1 for every chain: state0.H is still NaN when it runs
+        // (HMC.jl:214 ctor, HMCDA.jl:86-92), so p = NaN, a = -1 and the while loop never runs.
+        HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, 1.0, st));
+        HIP_TRY(mcmc_fill_f64(c->st.t_bar, c->C, 1.0, st));     // dualLeapStep = 1.
+        HIP_TRY(mcmc_fill_f64(c->st.t_h, c->C, 0.0, st));       // dualH = 0.
+    }
+    if (sa.tuner) {
+        HIP_TRY(mcmc_fill_i32(c->st.t_acc, c->C, 0, st));
+        HIP_TRY(mcmc_fill_i32(c->st.t_prop, c->C, 0, st));
+    }
+    int32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, ctx->d_err, sizeof err, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (err) return fail(MCMC_E_INIT_OUT_OF_SUPPORT, "Initial values out of model support, try other values");
+    c->steps_done = 0;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int64_t nchains, int64_t chain_offset,
+                                  uint64_t seed, const double* init_x, mcmc_chains** out) {
+    if (!m || !s || !out) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (int r = mcmc_sampler_validate(s)) return r;
+    if (nchains <= 0) return fail(MCMC_E_INVALID_ARG, "nchains should be > 0");
+    if (chain_offset < 0 || chain_offset + nchains > (int64_t)0x100000000LL)
+        return fail(MCMC_E_INVALID_ARG, "global chain ids must fit in 32 bits");
+    if (s->kind != MCMC_RWM && !m->has_gradient) {
+        const char* nm = s->kind == MCMC_MALA ? "MALA" : s->kind == MCMC_HMC ? "HMC" : "HMCDA";
+        return fail(MCMC_E_NEEDS_GRADIENT, std::string(nm) + " sampler requires model with gradient function");
+    }
+    mcmc_ctx* ctx = m->ctx;
+    if (int r = set_device(ctx)) return r;
+    const int d = m->args.d;
+    if (!model_is_separable(m) || d > mcmc_lpc_max_d())
+        return fail(MCMC_E_UNSUPPORTED, "this model x size combination is not built yet");
+    auto* c = new mcmc_chains();
+    c->model = m;
+    c->C = nchains;
+    c->ld = round_up(nchains, 64);
+    c->offset = chain_offset;
+    c->seed = seed;
+    c->layout = LAYOUT_LPC;
+    SamplerArgs& sa = c->sa;
+    sa.kind = s->kind;
+    sa.tuner = s->tuner;
+    sa.scale = s->scale;
+    sa.drift_step = s->drift_step;
+    sa.n_leaps = s->n_leaps;
+    sa.leap_step = s->leap_step;
+    sa.rate = s->rate;
+    sa.len = s->len;
+    sa.shrinkage = s->shrinkage;
+    sa.t0 = s->t0;
+    sa.step = s->step;
+    sa.adapt_step = s->adapt_step;
+    sa.max_step = s->max_step;
+    sa.target_path = s->target_path;
+    sa.target_rate = s->target_rate;
+    sa.max_leaps = s->max_leaps > 0 ? s->max_leaps : (int64_t)1 << 20;
+    auto bail = [&](int code) {
+        mcmc_chains_destroy(c);
+        return code;
+    };
+    const size_t ld = (size_t)c->ld;
+    if (int r = dmalloc(&c->st.x, (size_t)d * ld)) return bail(r);
+    if (int r = dmalloc(&c->st.lp, ld)) return bail(r);
+    const bool tuned = sa.tuner && (sa.kind == SK_MALA || sa.kind == SK_HMC);
+    if (tuned || sa.kind == SK_HMCDA)
+        if (int r = dmalloc(&c->st.t_step, ld)) return bail(r);
+    if (sa.kind == SK_HMCDA) {
+        if (int r = dmalloc(&c->st.t_bar, ld)) return bail(r);
+        if (int r = dmalloc(&c->st.t_h, ld)) return bail(r);
+    }
+    if (tuned) {
+        if (sa.kind == SK_HMC)
+            if (int r = dmalloc(&c->st.t_leaps, ld)) return bail(r);
+        if (int r = dmalloc(&c->st.t_acc, ld)) return bail(r);
+        if (int r = dmalloc(&c->st.t_prop, ld)) return bail(r);
+    }
+    // scale = model.scale .* sampler.scale (RWM.jl:52); other samplers do not use it.
+    std::vector<double> se(m->scale);
+    if (sa.kind == SK_RWM)
+        for (auto& v : se) v = v * sa.scale;
+    if (int r = dmalloc(&c->d_scale_eff, (size_t)d)) return bail(r);
+    if (hipMemcpy(c->d_scale_eff, se.data(), (size_t)d * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(MCMC_E_HIP, "scale upload failed"));
+    if (init_x) {
+        if (int r = dmalloc(&c->d_init_x, (size_t)d * ld)) return bail(r);
+        if (hipMemcpy2D(c->d_init_x, ld * 8, init_x, (size_t)nchains * 8, (size_t)nchains * 8, (size_t)d,
+                        hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(MCMC_E_HIP, "init_x upload failed"));
+    }
+    if (int r = init_state(c)) return bail(r);
+    *out = c;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_chains_destroy(mcmc_chains* c) {
+    if (!c) return MCMC_OK;
+    (void)hipSetDevice(c->model->ctx->device);
+    (void)hipStreamSynchronize(c->model->ctx->stream);
+    free_state(c);
+    dfree(c->d_scale_eff);
+    dfree(c->d_init_x);
+    dfree(c->out_samples.p);
+    dfree(c->out_grads.p);
+    dfree(c->out_bits.p);
+    dfree(c->out_tmp.p);
+    delete c;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_chains_reset(mcmc_chains* c) {
+    if (!c) return fail(MCMC_E_INVALID_ARG, "chains is NULL");
+    if (int r = set_device(c->model->ctx)) return r;
+    return init_state(c);
+}
+
+extern "C" int mcmc_chains_steps_done(mcmc_chains* c, int64_t* steps) {
+    if (!c || !steps) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    *steps = c->steps_done;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_chains_set_steps_per_launch(mcmc_chains* c, int64_t spl) {
+    if (!c || spl < 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    c->spl = spl;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_chains_set_store_gradients(mcmc_chains* c, int32_t store) {
+    if (!c) return fail(MCMC_E_INVALID_ARG, "chains is NULL");
+    c->store_grads = store ? 1 : 0;
+    return MCMC_OK;
+}
+
+// ------------------------------------------------------------------ run
+extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs* out) {
+    if (!c || !r) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    if (int rc = mcmc_runner_validate(r)) return rc;
+    mcmc_model* m = c->model;
+    mcmc_ctx* ctx = m->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    hipStream_t st = ctx->stream;
+    const int d = m->args.d;
+    const int64_t C = c->C;
+    const int64_t nkept = nkept_of(*r);
+    const int64_t nw = (C + 63) / 64;
+    if (c->steps_done + r->len > 0xffffffffLL) return fail(MCMC_E_INVALID_ARG, "step counter exceeds 2^32");
+    const bool on_dev = out && out->on_device;
+    const bool want_samples = out && out->samples;
+    const bool grad_sampler = c->sa.kind != SK_RWM;
+    const bool want_grads = out && out->gradients && grad_sampler && c->store_grads;
+    const bool want_bits = out && out->accept_bits;
+
+    double* d_samples = nullptr;
+    double* d_grads = nullptr;
+    uint64_t* d_bits = nullptr;
+    const size_t nsamp = (size_t)nkept * (size_t)d * (size_t)C;
+    if (want_samples) {
+        if (on_dev) d_samples = out->samples;
+        else {
+            if (int rc = ensure(c->out_samples, nsamp * 8)) return rc;
+            d_samples = (double*)c->out_samples.p;
+        }
+    }
+    if (want_grads) {
+        if (on_dev) d_grads = out->gradients;
+        else {
+            if (int rc = ensure(c->out_grads, nsamp * 8)) return rc;
+            d_grads = (double*)c->out_grads.p;
+        }
+    }
+    if (want_bits) {
+        if (on_dev) d_bits = out->accept_bits;
+        else {
+            if (int rc = ensure(c->out_bits, (size_t)nkept * nw * 8)) return rc;
+            d_bits = (uint64_t*)c->out_bits.p;
+        }
+    }
+
+    LpcArgs a = base_args(m, C, c->ld);
+    a.sa = c->sa;
+    a.st = c->st;
+    StepArgs& s = a.s;
+    s.chain0 = (uint32_t)c->offset;
+    s.key0 = (uint32_t)c->seed;
+    s.key1 = (uint32_t)(c->seed >> 32);
+    s.run_step0 = c->steps_done;
+    s.burnin = r->burnin;
+    s.thinning = r->thinning;
+    s.len = r->len;
+    s.tuner_burnin = r->burnin;
+    s.scale = c->d_scale_eff;
+    s.samples = d_samples;
+    s.grads = d_grads;
+    s.acc_bits = d_bits;
+    s.nw = nw;
+
+    const int64_t spl = c->spl > 0 ? c->spl : r->len;
+    HIP_TRY(hipStreamSynchronize(st));
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    for (int64_t done = 0; done < r->len; done += spl) {
+        const int64_t n = std::min(spl, r->len - done);
+        s.step_begin = c->steps_done + done + 1;
+        s.nsteps = (int32_t)n;
+        HIP_TRY(mcmc_launch_lpc_step(a, st));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    auto t1 = std::chrono::steady_clock::now();
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    c->steps_done += r->len;
+
+    if (out) {
+        out->nkept = nkept;
+        out->runtime_s = std::chrono::duration<double>(t1 - t0).count();
+        out->kernel_ms = ms;
+        if (!on_dev) {
+            if (want_samples) HIP_TRY(hipMemcpy(out->samples, d_samples, nsamp * 8, hipMemcpyDeviceToHost));
+            if (want_grads) HIP_TRY(hipMemcpy(out->gradients, d_grads, nsamp * 8, hipMemcpyDeviceToHost));
+            if (want_bits) HIP_TRY(hipMemcpy(out->accept_bits, d_bits, (size_t)nkept * nw * 8, hipMemcpyDeviceToHost));
+        }
+        if (out->final_x) {
+            if (on_dev) HIP_TRY(mcmc_copy_cols(out->final_x, C, c->st.x, c->ld, d, C, st));
+            else HIP_TRY(hipMemcpy2D(out->final_x, (size_t)C * 8, c->st.x, (size_t)c->ld * 8, (size_t)C * 8, (size_t)d,
+                                     hipMemcpyDeviceToHost));
+        }
+        if (out->final_lp)
+            HIP_TRY(hipMemcpy(out->final_lp, c->st.lp, (size_t)C * 8,
+                              on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return MCMC_OK;
+}
+
+// ------------------------------------------------------------------ debug probes
+extern "C" int mcmc_debug_detmath(mcmc_ctx* ctx, int op, int64_t n, const double* x, const double* y, double* out) {
+    if (!ctx || !x || !out || n <= 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    if (int r = set_device(ctx)) return r;
+    const size_t nout = (op == 6) ? 4 * (size_t)n : (size_t)n;
+    double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    int rc = MCMC_OK;
+    do {
+        if ((rc = dmalloc(&dx, (size_t)n))) break;
+        if ((rc = dmalloc(&dy, (size_t)n))) break;
+        if ((rc = dmalloc(&dout, nout))) break;
+        hipError_t e = hipMemcpy(dx, x, (size_t)n * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess && y) e = hipMemcpy(dy, y, (size_t)n * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = mcmc_detmath(op, n, dx, dy, dout, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = hipMemcpy(out, dout, nout * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("detmath probe: ") + hipGetErrorString(e));
+    } while (0);
+    dfree(dx);
+    dfree(dy);
+    dfree(dout);
+    return rc;
+}
+
+extern "C" int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+    if (!ctx || !ctr || !key || !out || n <= 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    if (int r = set_device(ctx)) return r;
+    uint32_t *dc = nullptr, *dk = nullptr, *dout = nullptr;
+    int rc = MCMC_OK;
+    do {
+        if ((rc = dmalloc(&dc, 4 * (size_t)n))) break;
+        if ((rc = dmalloc(&dk, 2 * (size_t)n))) break;
+        if ((rc = dmalloc(&dout, 4 * (size_t)n))) break;
+        hipError_t e = hipMemcpy(dc, ctr, 16 * (size_t)n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dk, key, 8 * (size_t)n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = mcmc_philox(n, dc, dk, dout, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = hipMemcpy(out, dout, 16 * (size_t)n, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("philox probe: ") + hipGetErrorString(e));
+    } while (0);
+    dfree(dc);
+    dfree(dk);
+    dfree(dout);
+    return rc;
+}

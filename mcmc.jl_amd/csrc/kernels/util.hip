@@ -1,0 +1,118 @@
+// util.hip -- small device helpers: fills, layout transposes and the
+// deterministic-math probes used by the parity tests (tests/test_gpu_detmath.py).
+#include "../common.hpp"
+#include "../detmath.hpp"
+
+namespace mcmc {
+
+__global__ void k_fill_f64(double* p, int64_t n, double v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+// dst[j][c] (stride ldd) <- v[j] for c < C  (every chain starts at model.init, RWM.jl:53)
+__global__ void k_broadcast_cols(double* dst, int64_t ldd, const double* v, int d, int64_t C) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    for (int j = 0; j < d; ++j) dst[(size_t)j * ldd + c] = v[j];
+}
+// dst[j][c] (stride ldd) <- src[j][c] (stride lds)
+__global__ void k_copy_cols(double* dst, int64_t ldd, const double* src, int64_t lds, int d, int64_t C) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    for (int j = 0; j < d; ++j) dst[(size_t)j * ldd + c] = src[(size_t)j * lds + c];
+}
+// Tiled transpose of R x S row-major matrices, batched: dst[b][s][r] <- src[b][r][s].
+__global__ void k_transpose(double* dst, const double* src, int64_t R, int64_t S) {
+    __shared__ double tile[32][33];
+    const int64_t b = blockIdx.z;
+    const int64_t r0 = (int64_t)blockIdx.y * 32, s0 = (int64_t)blockIdx.x * 32;
+    const double* sb = src + (size_t)b * R * S;
+    double* db = dst + (size_t)b * R * S;
+    for (int k = threadIdx.y; k < 32; k += blockDim.y) {
+        const int64_t r = r0 + k, s = s0 + threadIdx.x;
+        if (r < R && s < S) tile[k][threadIdx.x] = sb[(size_t)r * S + s];
+    }
+    __syncthreads();
+    for (int k = threadIdx.y; k < 32; k += blockDim.y) {
+        const int64_t s = s0 + k, r = r0 + threadIdx.x;
+        if (r < R && s < S) db[(size_t)s * R + r] = tile[threadIdx.x][k];
+    }
+}
+
+__global__ void k_detmath(int op, int64_t n, const double* x, const double* y, double* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double a = x[i];
+    double r = 0.0;
+    switch (op) {
+        case 0: r = det_log(a); break;
+        case 1: r = det_exp(a); break;
+        case 2: { double s, c; det_sincos2pi(a, s, c); r = s; } break;
+        case 3: { double s, c; det_sincos2pi(a, s, c); r = c; } break;
+        case 4: r = __builtin_sqrt(a); break;
+        case 5: r = a / y[i]; break;
+        case 6: {
+            // x[i] holds (chain, step, block) packed: chain = bits 0-31 of the integer value, step = y[i]
+            const uint64_t packed = (uint64_t)a;
+            const u32x4 w = philox4x32_10((uint32_t)packed, (uint32_t)y[i], (uint32_t)(packed >> 32), TAG_NORMAL,
+                                          0u, 0u);
+            double z0, z1, z2, z3;
+            normals4(w, z0, z1, z2, z3);
+            out[4 * i] = z0; out[4 * i + 1] = z1; out[4 * i + 2] = z2; out[4 * i + 3] = z3;
+            return;
+        }
+        case 7: r = round_away(a); break;
+        case 8: { const u32x4 w = philox4x32_10((uint32_t)(uint64_t)a, 0u, 0u, TAG_ACCEPT, 0u, 0u);
+                  r = uniform53(w.x, w.y); } break;
+        default: r = 0.0;
+    }
+    out[i] = r;
+}
+
+__global__ void k_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32x4 w = philox4x32_10(ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3], key[2 * i], key[2 * i + 1]);
+    out[4 * i] = w.x; out[4 * i + 1] = w.y; out[4 * i + 2] = w.z; out[4 * i + 3] = w.w;
+}
+
+}  // namespace mcmc
+
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    mcmc::k_fill_f64<<<nblk(n, 256), 256, 0, st>>>(p, n, v);
+    return hipGetLastError();
+}
+hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    mcmc::k_fill_i32<<<nblk(n, 256), 256, 0, st>>>(p, n, v);
+    return hipGetLastError();
+}
+hipError_t mcmc_broadcast_cols(double* dst, int64_t ldd, const double* v, int d, int64_t C, hipStream_t st) {
+    mcmc::k_broadcast_cols<<<nblk(C, 256), 256, 0, st>>>(dst, ldd, v, d, C);
+    return hipGetLastError();
+}
+hipError_t mcmc_copy_cols(double* dst, int64_t ldd, const double* src, int64_t lds, int d, int64_t C, hipStream_t st) {
+    mcmc::k_copy_cols<<<nblk(C, 256), 256, 0, st>>>(dst, ldd, src, lds, d, C);
+    return hipGetLastError();
+}
+hipError_t mcmc_transpose(double* dst, const double* src, int64_t batch, int64_t R, int64_t S, hipStream_t st) {
+    if (batch <= 0 || R <= 0 || S <= 0) return hipSuccess;
+    const dim3 grid(nblk(S, 32), nblk(R, 32), (unsigned)batch);
+    mcmc::k_transpose<<<grid, dim3(32, 8), 0, st>>>(dst, src, R, S);
+    return hipGetLastError();
+}
+hipError_t mcmc_detmath(int op, int64_t n, const double* x, const double* y, double* out, hipStream_t st) {
+    mcmc::k_detmath<<<nblk(n, 256), 256, 0, st>>>(op, n, x, y, out);
+    return hipGetLastError();
+}
+hipError_t mcmc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out, hipStream_t st) {
+    mcmc::k_philox<<<nblk(n, 256), 256, 0, st>>>(n, ctr, key, out);
+    return hipGetLastError();
+}

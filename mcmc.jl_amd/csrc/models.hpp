@@ -1,0 +1,67 @@
+// models.hpp -- separable log-targets of the model catalogue, device side.
+//
+// The reference evaluates user closures (likmodel.jl:21,25) or DSL-generated
+// code (modelparser.jl:39-104).  Across the C ABI the model is a catalogue
+// entry; each entry restates the arithmetic of its reference definition:
+//
+//   IsoDot     model(v -> -dot(v,v), grad = v -> -2v)   README.md:60,63;
+//              test/test_syntax.jl:40-41.  A function model: no LLAcc rule,
+//              the closure's value is used as is (likmodel.jl:100-143).
+//   NormalDSL  :(v ~ Normal(mu, sigma)), gradient=true  README.md:67-72.
+//              lp = LLAcc(0.) + sum(logpdf(Normal(mu,sigma), v)) and a
+//              non-finite running sum throws OutOfSupportError, which the
+//              generated function turns into (-Inf, zero(beta))
+//              (AccumulatorDerivRules.jl:14-16, modelparser.jl:64-72).
+//              Gradient rule dx += (mu - x)/(sigma*sigma) * ds (MCMCDerivRules.jl:57).
+//
+// Summation: the reference sums with BLAS ddot / Julia `sum`; the build fixes
+// the order so that the oracle can restate it exactly: lane-per-chain kernels
+// sum left to right over j; wave-per-chain kernels sum each lane's coordinates
+// in order and then combine the 64 lane partials by an xor butterfly
+// (DESIGN.md §4).  Accumulation is `acc = fma(v, v, acc)` for the dot product
+// and `acc = acc + term` for logpdf sums.
+#pragma once
+#include "common.hpp"
+#include "detmath.hpp"
+
+namespace mcmc {
+
+constexpr double kLog2Pi = 0x1.d67f1c864beb5p+0;   // log(2*pi) rounded
+constexpr double kTwoPi = 0x1.921fb54442d18p+2;    // 2*pi rounded (Julia 2*pi)
+
+struct IsoDot {
+    static constexpr bool kLLAcc = false;
+    __device__ explicit IsoDot(const ModelArgs&) {}
+    __device__ __forceinline__ void acc(double& a, double v) const { a = __builtin_fma(v, v, a); }
+    __device__ __forceinline__ double finish(double a) const { return -a; }
+    __device__ __forceinline__ double grad(double v) const { return -2.0 * v; }
+};
+
+struct NormalDSL {
+    static constexpr bool kLLAcc = true;
+    double mu, sigma, logsig, s2;
+    __device__ explicit NormalDSL(const ModelArgs& m) : mu(m.mu), sigma(m.sigma) {
+        logsig = det_log(sigma);
+        s2 = sigma * sigma;
+    }
+    __device__ __forceinline__ void acc(double& a, double v) const {
+        const double z = (v - mu) / sigma;
+        a = a + (-0.5 * (z * z + kLog2Pi) - logsig);
+    }
+    __device__ __forceinline__ double finish(double a) const { return a; }
+    __device__ __forceinline__ double grad(double v) const { return (mu - v) / s2; }
+};
+
+// LLAcc rule: a non-finite total means out of support -> (-Inf, 0).
+template <class M>
+__device__ __forceinline__ double llacc_finish(const M& m, double a, bool& oos) {
+    double lp = m.finish(a);
+    oos = false;
+    if (M::kLLAcc) {
+        oos = !(lp - lp == 0.0);      // !isfinite(lp)
+        if (oos) lp = -__builtin_inf();
+    }
+    return lp;
+}
+
+}  // namespace mcmc

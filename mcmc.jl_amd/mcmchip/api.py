@@ -1,0 +1,546 @@
+"""Host-side mirror of MCMC.jl's model x sampler x runner API, driving the C ABI.
+
+Names, argument meaning and error behaviour follow the reference:
+
+  model(f; init, scale, grad)    src/modellers/mcmcmodels.jl:27-33, likmodel.jl:100-143
+  RWM, MALA, HMC, HMCDA          src/samplers/{RWM,MALA,HMC,HMCDA}.jl (constructors + @asserts)
+  EmpMCTuner                     src/samplers/samplers.jl:32-50
+  SerialMC(steps, burnin, thinning) / SerialMC(range)   src/runners/SerialMC.jl:12-35
+  m * s * r -> MCMCTask          src/MCMC.jl:87-98
+  run(task) / run(chain)         src/runners/runners.jl:7-14,45 ; SerialMC.jl:37-85
+  resume(chain; steps)           src/runners/runners.jl:48-68 ; SerialMC.jl:93-97
+  MCMCChain                      src/MCMC.jl:58-84
+
+What is new: one MCMCTask is a *batch* of `nchains` independent Markov chains
+of the same (model, sampler, runner) -- the reference's `run(Array{MCMCTask})`
+(runners.jl:17-26) for the homogeneous case -- each chain with its own random
+stream keyed by (seed, global chain id, step).  Julia closures cannot cross a
+C ABI, so `model()` takes an entry of the model catalogue (IsoNormalDot,
+NormalDSL, LogisticRegression, LinearRegression) in place of a function.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import math
+from typing import Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dptr
+
+__all__ = [
+    "IsoNormalDot", "NormalDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
+    "RWM", "MALA", "HMC", "HMCDA", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
+    "run", "resume", "device_count",
+]
+
+# ------------------------------------------------------------------ device contexts
+_CTX: dict = {}
+
+
+def device_count() -> int:
+    n = ct.c_int(0)
+    check(_lib.load().mcmc_device_count(ct.byref(n)))
+    return n.value
+
+
+def _ctx(device: int) -> ct.c_void_p:
+    if device not in _CTX:
+        h = ct.c_void_p()
+        check(_lib.load().mcmc_ctx_create(int(device), ct.byref(h)))
+        _CTX[device] = h
+    return _CTX[device]
+
+
+def _f64(a, n: Optional[int] = None) -> np.ndarray:
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if n is not None and arr.shape != (n,):
+        raise ValueError(f"expected a vector of length {n}, got shape {arr.shape}")
+    return arr
+
+
+# ------------------------------------------------------------------ model catalogue
+class IsoNormalDot:
+    """The README target `v -> -dot(v,v)`; its gradient `v -> -2v` is `IsoNormalDot.grad` (README.md:60,63)."""
+    kind = _lib.MODEL_ISO_NORMAL_DOT
+    grad = "v -> -2v"
+
+
+class NormalDSL:
+    """The DSL model `v ~ Normal(mu, sigma)` with gradient=true (README.md:67-72)."""
+    kind = _lib.MODEL_NORMAL_DSL
+
+    def __init__(self, mu: float = 0.0, sigma: float = 1.0):
+        self.mu, self.sigma = float(mu), float(sigma)
+
+
+class LogisticRegression:
+    """examples/logistic_regression.jl:16-22: vars ~ Normal(0, prior); prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob).
+    link_sign=-1 gives test/test_syntax.jl:13's exp(+X*vars) variant."""
+    kind = _lib.MODEL_LOGISTIC
+
+    def __init__(self, X, Y, prior_sigma: float = 1.0, link_sign: float = 1.0):
+        self.X = np.ascontiguousarray(np.asarray(X, dtype=np.float64))
+        self.Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
+        self.prior_sigma, self.link_sign = float(prior_sigma), float(link_sign)
+
+
+class LinearRegression:
+    """examples/linear_regression.jl:14-20: vars ~ Normal(0, prior); resid = Y - X*vars; resid ~ Normal(0, noise)."""
+    kind = _lib.MODEL_LINEAR
+
+    def __init__(self, X, Y, prior_sigma: float = 1.0, noise_sigma: float = 1.0):
+        self.X = np.ascontiguousarray(np.asarray(X, dtype=np.float64))
+        self.Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
+        self.prior_sigma, self.noise_sigma = float(prior_sigma), float(noise_sigma)
+
+
+class MCMCLikelihoodModel:
+    """MCMCLikelihoodModel (likmodel.jl:20-57): target + init + scale + pmap, uploaded once per GPU."""
+
+    def __init__(self, target, init, scale=1.0, gradient: bool = False, pmap: Optional[dict] = None):
+        self.target = target
+        init = [float(init)] if np.isscalar(init) else init                   # likmodel.jl:112
+        self.init = _f64(init).reshape(-1)
+        self.size = int(self.init.shape[0])
+        if np.isscalar(scale):
+            self.scale = float(scale) * np.ones(self.size)                     # likmodel.jl:115
+        else:
+            self.scale = _f64(scale).reshape(-1)
+        if self.scale.shape[0] != self.size:                                   # likmodel.jl:44
+            raise AssertionError(f"scale parameter size ({self.scale.shape[0]}) different from initial values "
+                                 f"({self.size})")
+        self.has_gradient = bool(gradient)         # hasgradient(m) = m.evalg != nothing (mcmcmodels.jl:19)
+        self.pmap = pmap if pmap is not None else {"pars": (1, (self.size,))}  # likmodel.jl:118
+        if hasattr(target, "X"):
+            if target.X.ndim != 2 or target.X.shape[1] != self.size:
+                raise ValueError(f"X must be [n, {self.size}]")
+            if target.Y.shape != (target.X.shape[0],):
+                raise ValueError("Y must have one entry per row of X")
+        self._dev: dict = {}
+
+    # device handle, created on first use per GPU
+    def _handle(self, device: int) -> ct.c_void_p:
+        if device in self._dev:
+            return self._dev[device]
+        t = self.target
+        desc = _lib.ModelDesc()
+        desc.kind = t.kind
+        desc.has_gradient = 1 if self.has_gradient else 0
+        desc.d = self.size
+        desc.init = dptr(self.init)
+        desc.scale = dptr(self.scale)
+        desc.mu = getattr(t, "mu", 0.0)
+        desc.sigma = getattr(t, "sigma", 1.0)
+        desc.prior_sigma = getattr(t, "prior_sigma", 1.0)
+        desc.noise_sigma = getattr(t, "noise_sigma", 1.0)
+        desc.link_sign = getattr(t, "link_sign", 1.0)
+        if hasattr(t, "X"):
+            desc.n = t.X.shape[0]
+            desc.X = dptr(t.X)
+            desc.Y = dptr(t.Y)
+        h = ct.c_void_p()
+        check(_lib.load().mcmc_model_create(_ctx(device), ct.byref(desc), ct.byref(h)))
+        self._dev[device] = h
+        return h
+
+    def eval(self, x, device: int = 0):
+        """model.eval on a batch: x [d] or [d, nchains] -> lp (likmodel.jl:21)."""
+        return self.evalallg(x, device=device, _grad=False)[0]
+
+    def evalallg(self, x, device: int = 0, _grad: bool = True):
+        """model.evalallg on a batch: x [d] or [d, nchains] -> (lp, grad) (likmodel.jl:25)."""
+        xa = np.asarray(x, dtype=np.float64)
+        single = xa.ndim == 1
+        xa = np.ascontiguousarray(xa.reshape(self.size, -1))
+        C = xa.shape[1]
+        lp = np.empty(C)
+        g = np.empty((self.size, C)) if _grad else None
+        check(_lib.load().mcmc_model_eval(self._handle(device), C, dptr(xa), dptr(lp), dptr(g)))
+        if single:
+            return lp[0], (g[:, 0] if g is not None else None)
+        return lp, g
+
+    def __mul__(self, sampler):
+        return _ModelSampler(self, sampler)
+
+    def __del__(self):
+        try:
+            lib = _lib.load()
+            for h in self._dev.values():
+                lib.mcmc_model_destroy(h)
+        except Exception:
+            pass
+
+
+def model(f, mtype: str = "likelihood", init=None, scale=1.0, gradient: bool = False,
+          grad=None, **dsl_init) -> MCMCLikelihoodModel:
+    """model() entry point (mcmcmodels.jl:27-33).
+
+    Function style (likmodel.jl:100-143): model(IsoNormalDot(), init=ones(3)) has no gradient, like
+    `model(v-> -dot(v,v), init=ones(3))`; pass grad=IsoNormalDot.grad (or grad=True) for mymodel2's
+    `grad=v->-2v` (README.md:60-63).  DSL style (likmodel.jl:72-96): model(NormalDSL(0, 1), v=ones(3),
+    gradient=True), model(LogisticRegression(X, Y), vars=zeros(10), gradient=True)."""
+    if mtype != "likelihood":
+        raise ValueError(f"unknown model type {mtype!r}")
+    if dsl_init:
+        if init is not None:
+            raise AssertionError("'init' kwargs not allowed for model as expression\n")   # likmodel.jl:80
+        # modelVars (expr_funcs.jl:76-90): parameters packed column-major, concatenated in keyword order
+        init = np.concatenate([np.asarray(v, dtype=np.float64).reshape(-1, order="F") for v in dsl_init.values()])
+    if init is None:
+        init = [1.0]                                                                       # likmodel.jl:107
+    if grad is not None and grad is not False:
+        gradient = True
+    return MCMCLikelihoodModel(f, init, scale=scale, gradient=gradient)
+
+
+# ------------------------------------------------------------------ samplers
+class EmpiricalMCMCTuner:
+    """EmpiricalMCMCTuner (samplers.jl:32-50)."""
+
+    def __init__(self, targetRate: float, adaptStep: int = 100, maxStep: int = 200, targetPath: float = 1.0,
+                 verbose: bool = False):
+        if not adaptStep > 0:
+            raise AssertionError(f"Adaptation step size ({adaptStep}) should be > 0")
+        if not maxStep > 0:
+            raise AssertionError(f"Adaptation step size ({maxStep}) should be > 0")
+        if not 0 < targetRate < 1:
+            raise AssertionError(f"Target acceptance rate ({targetRate}) should be between 0 and 1")
+        self.targetRate, self.adaptStep, self.maxStep = float(targetRate), int(adaptStep), int(maxStep)
+        self.targetPath, self.verbose = float(targetPath), bool(verbose)
+
+
+EmpMCTuner = EmpiricalMCMCTuner
+
+
+class _Sampler:
+    kind = 0
+    tuner = None
+
+    def cfg(self) -> _lib.SamplerCfg:
+        c = _lib.SamplerCfg()
+        c.kind = self.kind
+        t = self.tuner
+        if t is not None:
+            c.tuner = 1
+            c.adapt_step, c.max_step = t.adaptStep, t.maxStep
+            c.target_path, c.target_rate = t.targetPath, t.targetRate
+        return c
+
+    def __mul__(self, runner):                     # sampler * runner (for model * (sampler * runner) chains)
+        return _SamplerRunner(self, runner)
+
+
+class RWM(_Sampler):
+    """Random-walk Metropolis (RWM.jl:24-36)."""
+    kind = _lib.SAMPLER_RWM
+
+    def __init__(self, scale: float = 1.0, tuner=None):
+        if not scale > 0:
+            raise AssertionError("scale should be > 0")                       # RWM.jl:29
+        if tuner is not None:
+            raise NotImplementedError("RWMTuner is abstract in the reference (RWM.jl:18)")
+        self.scale = float(scale)
+
+    def cfg(self):
+        c = super().cfg()
+        c.scale = self.scale
+        return c
+
+
+class MALA(_Sampler):
+    """Metropolis-adjusted Langevin (MALA.jl:50-62)."""
+    kind = _lib.SAMPLER_MALA
+
+    def __init__(self, driftStep: Union[float, EmpiricalMCMCTuner] = 1.0, tuner=None, scale: Optional[float] = None):
+        if isinstance(driftStep, EmpiricalMCMCTuner):          # MALA(s::MCMCTuner) = MALA(1.0, t)
+            driftStep, tuner = 1.0, driftStep
+        if scale is not None:                                  # MALA(;scale, tuner) keyword form
+            driftStep = scale
+        if not driftStep > 0:
+            raise AssertionError("MALA drift step should be > 0")              # MALA.jl:55
+        self.driftStep, self.tuner = float(driftStep), tuner
+
+    def cfg(self):
+        c = super().cfg()
+        c.drift_step = self.driftStep
+        return c
+
+
+class HMC(_Sampler):
+    """Hamiltonian Monte Carlo (HMC.jl:53-74); positional forms as the reference's constructors:
+    HMC(), HMC(nLeaps), HMC(nLeaps, leapStep), HMC(leapStep::Float64), HMC(tuner)."""
+    kind = _lib.SAMPLER_HMC
+
+    def __init__(self, *args, nLeaps: Optional[int] = None, leapStep: Optional[float] = None, tuner=None,
+                 storeLeaps: bool = False):
+        n, e = 10, 0.1
+        a = list(args)
+        if a and isinstance(a[-1], EmpiricalMCMCTuner):
+            tuner = a.pop()
+        if len(a) == 1:
+            if isinstance(a[0], float):
+                e = a[0]                                        # HMC(leapStep::Float64) = HMC(10, leapStep)
+            else:
+                n = int(a[0])                                   # HMC(nLeaps::Int) = HMC(nLeaps, 0.1)
+        elif len(a) == 2:
+            n, e = int(a[0]), float(a[1])
+        elif len(a) > 2:
+            raise TypeError("HMC(nLeaps, leapStep[, tuner])")
+        if nLeaps is not None:
+            n = int(nLeaps)
+        if leapStep is not None:
+            e = float(leapStep)
+        if not n > 0:
+            raise AssertionError("inner steps should be > 0")                  # HMC.jl:60
+        if not e > 0:
+            raise AssertionError("inner steps scaling should be > 0")          # HMC.jl:61
+        if storeLeaps:
+            raise NotImplementedError("storeLeaps diagnostics are not produced by the batched kernels")
+        self.nLeaps, self.leapStep, self.tuner = n, e, tuner
+
+    def cfg(self):
+        c = super().cfg()
+        c.n_leaps, c.leap_step = self.nLeaps, self.leapStep
+        return c
+
+
+class HMCDA(_Sampler):
+    """HMC with dual-averaging step size (HMCDA.jl:24-43)."""
+    kind = _lib.SAMPLER_HMCDA
+
+    def __init__(self, rate: float = 0.65, len: float = 2.0, shrinkage: float = 0.05, t0: float = 10.0,
+                 step: float = 0.75, storeLeaps: bool = False, max_leaps: int = 0):
+        if not 0.0 < rate < 1.0:
+            raise AssertionError(f"Target acceptance rate ({rate}) should be between 0 and 1")
+        if not len > 0:
+            raise AssertionError(f"len parameter of HMCDA sampler ({len}) must be non-negative")
+        if not shrinkage > 0.0:
+            raise AssertionError(f"shrinkage parameter of HMCDA sampler ({shrinkage}) must be positive")
+        if not t0 >= 0:
+            raise AssertionError(f"t0 parameter of HMCDA sampler ({t0}) must be non-negative")
+        if storeLeaps:
+            raise NotImplementedError("storeLeaps diagnostics are not produced by the batched kernels")
+        self.rate, self.len, self.shrinkage, self.t0, self.step = rate, len, shrinkage, t0, step
+        self.max_leaps = int(max_leaps)
+
+    def cfg(self):
+        c = super().cfg()
+        c.rate, c.len, c.shrinkage, c.t0, c.step = self.rate, self.len, self.shrinkage, self.t0, self.step
+        c.max_leaps = self.max_leaps
+        return c
+
+
+# ------------------------------------------------------------------ runner
+class SerialMC:
+    """SerialMC runner (SerialMC.jl:12-35): keeps samples i in r = (burnin+1):thinning:steps."""
+
+    def __init__(self, steps: Union[int, range] = 100, burnin: int = 0, thinning: int = 1):
+        if isinstance(steps, range):                           # SerialMC(steps::Range)
+            r = steps
+            burnin = r.start - 1
+            thinning = r.step
+            length = r[-1] if len(r) else r.start - 1
+        else:
+            length = int(steps)
+        if not burnin >= 0:
+            raise AssertionError(f"Burnin rounds ({burnin}) should be >= 0")
+        if not length > burnin:
+            raise AssertionError(f"Total MCMC length ({length}) should be > to burnin ({burnin})")
+        if not thinning >= 1:
+            raise AssertionError(f"Thinning ({thinning}) should be >= 1")
+        self.burnin, self.thinning, self.len = int(burnin), int(thinning), int(length)
+        self.r = range(self.burnin + 1, self.len + 1, self.thinning)
+
+    def cfg(self) -> _lib.RunnerCfg:
+        c = _lib.RunnerCfg()
+        c.burnin, c.thinning, c.len = self.burnin, self.thinning, self.len
+        return c
+
+
+# ------------------------------------------------------------------ task / chain
+class _ModelSampler:
+    def __init__(self, m, s):
+        self.m, self.s = m, s
+
+    def __mul__(self, r):
+        return _spin(self.m, self.s, r)
+
+
+class _SamplerRunner:
+    def __init__(self, s, r):
+        self.s, self.r = s, r
+
+    def __rmul__(self, m):
+        return _spin(m, self.s, self.r)
+
+
+def _spin(m, s, r):
+    """m * s * r with the reference's array broadcasting (MCMC.jl:87-98)."""
+    ms = m if isinstance(m, (list, tuple)) else None
+    ss = s if isinstance(s, (list, tuple)) else None
+    rs = r if isinstance(r, (list, tuple)) else None
+    if ms is None and ss is None and rs is None:
+        return MCMCTask(m, s, r)
+    n = max(len(x) for x in (ms, ss, rs) if x is not None)
+    pick = lambda v, i: v[i] if isinstance(v, (list, tuple)) else v  # noqa: E731
+    return [MCMCTask(pick(m, i), pick(s, i), pick(r, i)) for i in range(n)]
+
+
+class MCMCTask:
+    """A batch of `nchains` independent chains of (model, sampler, runner) on one GPU (MCMC.jl:33-39)."""
+
+    def __init__(self, model: MCMCLikelihoodModel, sampler: _Sampler, runner: SerialMC, nchains: int = 1,
+                 seed: int = 1, device: int = 0, chain_offset: int = 0, init_x=None, steps_per_launch: int = 0):
+        self._h = None
+        if not isinstance(runner, SerialMC):
+            raise NotImplementedError("only the SerialMC runner drives the batched kernels")
+        if sampler.kind != _lib.SAMPLER_RWM and not model.has_gradient:
+            name = type(sampler).__name__
+            raise AssertionError(f"{name} sampler requires model with gradient function")
+        self.model, self.sampler, self.runner = model, sampler, runner
+        self.nchains, self.seed, self.device = int(nchains), int(seed), int(device)
+        self.chain_offset = int(chain_offset)
+        self.init_x = None if init_x is None else np.ascontiguousarray(
+            np.asarray(init_x, dtype=np.float64).reshape(model.size, self.nchains))
+        self.steps_per_launch = int(steps_per_launch)
+
+    def batch(self, nchains: int, seed: Optional[int] = None, **kw) -> "MCMCTask":
+        """Same (model, sampler, runner) over `nchains` chains."""
+        return MCMCTask(self.model, self.sampler, self.runner, nchains=nchains,
+                        seed=self.seed if seed is None else seed, device=kw.get("device", self.device),
+                        chain_offset=kw.get("chain_offset", self.chain_offset), init_x=kw.get("init_x"),
+                        steps_per_launch=kw.get("steps_per_launch", self.steps_per_launch))
+
+    def handle(self) -> ct.c_void_p:
+        if self._h is None:
+            mh = self.model._handle(self.device)
+            h = ct.c_void_p()
+            cfg = self.sampler.cfg()
+            check(_lib.load().mcmc_chains_create(mh, ct.byref(cfg), self.nchains, self.chain_offset,
+                                                 ct.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF),
+                                                 dptr(self.init_x), ct.byref(h)))
+            if self.steps_per_launch:
+                check(_lib.load().mcmc_chains_set_steps_per_launch(h, self.steps_per_launch))
+            self._h = h
+        return self._h
+
+    @property
+    def steps_done(self) -> int:
+        if self._h is None:
+            return 0
+        v = ct.c_int64(0)
+        check(_lib.load().mcmc_chains_steps_done(self._h, ct.byref(v)))
+        return v.value
+
+    def reset(self) -> None:
+        if self._h is not None:
+            check(_lib.load().mcmc_chains_reset(self._h))
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            try:
+                _lib.load().mcmc_chains_destroy(self._h)
+            except Exception:
+                pass
+
+
+class MCMCChain:
+    """Result of a run (MCMC.jl:58-80), batched over chains.
+
+    samples[c] is chain c's [nkept x d] sample matrix (the reference's DataFrame);
+    gradients likewise (all NaN for RWM, SerialMC.jl:42); diagnostics["accept"][c]
+    is the per-kept-step accept flag and diagnostics["step"] = collect(r)."""
+
+    def __init__(self, r: range, samples, gradients, diagnostics: dict, task: MCMCTask, runTime: float,
+                 kernel_ms: float = float("nan"), final_x=None, final_lp=None):
+        self.range = r
+        self._samples = samples                 # [nkept, d, nchains] (C ABI layout)
+        self._gradients = gradients
+        self.diagnostics = diagnostics
+        self.task = task
+        self.runTime = runTime
+        self.kernel_ms = kernel_ms
+        self.final_x, self.final_lp = final_x, final_lp
+
+    @property
+    def samples(self) -> np.ndarray:
+        return np.transpose(self._samples, (2, 0, 1))
+
+    @property
+    def gradients(self) -> np.ndarray:
+        if self._gradients is None:
+            nk, d, C = self._samples.shape
+            return np.full((C, nk, d), np.nan)
+        return np.transpose(self._gradients, (2, 0, 1))
+
+    @property
+    def nchains(self) -> int:
+        return self._samples.shape[2]
+
+    def __repr__(self) -> str:                                                 # MCMC.jl:82-84
+        nk, d, C = self._samples.shape
+        return f"{d} parameters, {nk} samples (per parameter), {C} chain(s), {round(self.runTime, 1)} sec."
+
+
+def _unpack_bits(bits: np.ndarray, C: int) -> np.ndarray:
+    """[nkept][ceil(C/64)] u64 -> bool [C, nkept]; bit c%64 of word c//64 is chain c."""
+    nk = bits.shape[0]
+    b = np.unpackbits(bits.view(np.uint8).reshape(nk, -1), axis=1, bitorder="little")[:, :C]
+    return b.astype(bool).T.copy()
+
+
+def _run_task(t: MCMCTask) -> MCMCChain:
+    lib = _lib.load()
+    h = t.handle()
+    r = t.runner
+    d, C = t.model.size, t.nchains
+    nk = len(r.r)
+    nw = (C + 63) // 64
+    samples = np.empty((nk, d, C))
+    grads = np.empty((nk, d, C)) if t.sampler.kind != _lib.SAMPLER_RWM else None
+    bits = np.zeros((nk, nw), dtype=np.uint64)
+    fx = np.empty((d, C))
+    flp = np.empty(C)
+    out = _lib.Outputs()
+    out.samples = samples.ctypes.data
+    out.gradients = grads.ctypes.data if grads is not None else None
+    out.accept_bits = bits.ctypes.data
+    out.final_x = fx.ctypes.data
+    out.final_lp = flp.ctypes.data
+    out.on_device = 0
+    cfg = r.cfg()
+    check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
+    diags = {"step": list(r.r), "accept": _unpack_bits(bits, C)}
+    return MCMCChain(r.r, samples, grads, diags, t, out.runtime_s, out.kernel_ms, fx, flp)
+
+
+def run(t, *args, nchains: Optional[int] = None, seed: Optional[int] = None, **kw):
+    """run(task) / run(chain) (continue) / run(m, s, r) / run([tasks])  (runners.jl:7-32,45)."""
+    if args:                                                 # run(m, s, r)
+        return run(_spin(t, args[0], args[1]), nchains=nchains, seed=seed, **kw)
+    if isinstance(t, (list, tuple)):
+        kinds = {type(x.runner if isinstance(x, MCMCTask) else x.task.runner) for x in t}
+        if len(kinds) != 1:
+            raise AssertionError("Runners do not have the same runner type")
+        return [run(x, nchains=nchains, seed=seed, **kw) for x in t]
+    if isinstance(t, MCMCChain):                              # run(c::MCMCChain) = run(c.task)
+        return _run_task(t.task)
+    if nchains is not None or seed is not None or kw:
+        if t._h is not None:
+            raise ValueError("task already started; build a new task to change nchains/seed")
+        t = t.batch(nchains if nchains is not None else t.nchains, seed=seed, **kw)
+    return _run_task(t)
+
+
+def resume(c, steps: int = 100):
+    """resume(chain; steps): a *new* task from model.init with SerialMC(steps, thinning) (SerialMC.jl:93-97)."""
+    if isinstance(c, (list, tuple)):
+        return [resume(x, steps=steps) for x in c]
+    t = c.task if isinstance(c, MCMCChain) else c
+    nt = MCMCTask(t.model, t.sampler, SerialMC(steps=steps, thinning=t.runner.thinning), nchains=t.nchains,
+                  seed=t.seed, device=t.device, chain_offset=t.chain_offset, init_x=t.init_x,
+                  steps_per_launch=t.steps_per_launch)
+    return _run_task(nt)

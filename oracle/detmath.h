@@ -1,0 +1,206 @@
+/*
+ * oracle/detmath.h -- TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
+ *
+ * CPU restatement of the build's random-number and fp64 math specification
+ * (DESIGN.md §3 "RNG and deterministic math").  The reference (MCMC.jl, Julia
+ * 0.2) draws with dSFMT + ziggurat `randn` / `rand` (src/samplers/RWM.jl:59,63)
+ * and evaluates `log`/`exp` with openlibm; neither can run here (no Julia), so
+ * the build defines its own counter-based stream and its own fp64 kernels, and
+ * this header restates them operation for operation, so that the HIP path and
+ * the oracle produce bit-identical draws and accept decisions.
+ *
+ *   Philox4x32-10 ..... Salmon et al., SC'11 (Random123); pinned by the
+ *                       Random123 known-answer vectors (tests/golden/philox_kat.json)
+ *   uniform53 ......... 53-bit uniform on [0,1)  (Julia `rand()` semantics: 0 possible, 1 not)
+ *   det_log ........... fdlibm e_log.c algorithm (Sun, 1993), branch-free general
+ *                       path, explicit fma in the polynomial
+ *   det_exp ........... Cody-Waite reduction + degree-13 Taylor (fma Horner)
+ *   det_sincos2pi ..... exact quarter-turn reduction + Taylor polynomials in r
+ *   Box-Muller ........ normals from 32-bit uniforms, 4 normals per Philox block
+ *
+ * Compile with -ffp-contract=off: every fused multiply-add is an explicit fma();
+ * no other product may be fused.  sqrt and '/' are IEEE correctly rounded.
+ */
+#ifndef MCMC_ORACLE_DETMATH_H
+#define MCMC_ORACLE_DETMATH_H
+
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+
+#define ORC_PHILOX_M0 0xD2511F53u
+#define ORC_PHILOX_M1 0xCD9E8D57u
+#define ORC_PHILOX_W0 0x9E3779B9u
+#define ORC_PHILOX_W1 0xBB67AE85u
+
+/* stream tags (counter word 3) */
+#define ORC_TAG_NORMAL 0u   /* proposal / momentum normals            */
+#define ORC_TAG_ACCEPT 1u   /* Metropolis-Hastings accept uniform      */
+#define ORC_TAG_DATA   7u   /* synthetic data generation (bench configs) */
+
+static inline void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += ORC_PHILOX_W0; k1 += ORC_PHILOX_W1; }
+        uint64_t p0 = (uint64_t)ORC_PHILOX_M0 * (uint64_t)c0;
+        uint64_t p1 = (uint64_t)ORC_PHILOX_M1 * (uint64_t)c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* One Philox block of the build's stream: counter = (chain, step, block, tag), key = seed. */
+static inline void orc_block(uint64_t seed, uint32_t chain, uint32_t step, uint32_t block,
+                             uint32_t tag, uint32_t out[4]) {
+    uint32_t ctr[4] = {chain, step, block, tag};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    orc_philox4x32_10(ctr, key, out);
+}
+
+static inline double orc_bits2d(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
+static inline uint64_t orc_d2bits(double d) { uint64_t b; memcpy(&b, &d, 8); return b; }
+
+/* 53-bit uniform on [0,1) from two 32-bit words. */
+static inline double orc_uniform53(uint32_t a, uint32_t b) {
+    uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return (double)m * 0x1p-53;
+}
+/* 32-bit uniform on (0,1): never 0, never 1. */
+static inline double orc_uniform32_open(uint32_t a) { return ((double)a + 0.5) * 0x1p-32; }
+/* 32-bit uniform on [0,1). */
+static inline double orc_uniform32(uint32_t a) { return (double)a * 0x1p-32; }
+
+/* 2^k for k in [-1022, 1023], built from bits. */
+static inline double orc_pow2i(int k) { return orc_bits2d((uint64_t)(k + 1023) << 52); }
+
+/* ---------------------------------------------------------------- log */
+static inline double orc_log(double x) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2,
+                 Lg3 = 0x1.2492494229359p-2, Lg4 = 0x1.c71c51d8e78afp-3,
+                 Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    if (x != x) return x;                                  /* NaN  */
+    if (x < 0.0) return orc_bits2d(0x7ff8000000000000ull); /* NaN  */
+    if (x == 0.0) return -INFINITY;
+    uint64_t bx = orc_d2bits(x);
+    if (bx >= 0x7ff0000000000000ull) return x;             /* +inf */
+    int k = 0;
+    if (bx < 0x0010000000000000ull) {                      /* subnormal: scale by 2^54 */
+        x = x * 0x1p54; k = -54; bx = orc_d2bits(x);
+    }
+    uint32_t hx = (uint32_t)(bx >> 32);
+    k += (int)(hx >> 20) - 1023;
+    hx &= 0x000fffffu;
+    uint32_t i = (hx + 0x95f64u) & 0x100000u;              /* != 0 iff mantissa >= sqrt(2) */
+    uint64_t nb = ((uint64_t)(hx | (i ^ 0x3ff00000u)) << 32) | (bx & 0xffffffffull);
+    double m = orc_bits2d(nb);                             /* m in [sqrt(2)/2, sqrt(2)) */
+    k += (int)(i >> 20);
+    double f = m - 1.0;
+    double s = f / (2.0 + f);
+    double dk = (double)k;
+    double z = s * s;
+    double w = z * z;
+    double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+    double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+    double R = t2 + t1;
+    double hfsq = 0.5 * f * f;
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* ---------------------------------------------------------------- exp */
+static inline double orc_exp(double x) {
+    const double inv_ln2 = 0x1.71547652b82fep+0;
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double shifter = 0x1.8p52;
+    if (x != x) return x;
+    if (x > 709.782712893384) return INFINITY;
+    if (x < -745.1332191019412) return 0.0;
+    double t = fma(x, inv_ln2, shifter);
+    double kd = t - shifter;                               /* nearest integer to x/ln2 */
+    int k = (int)kd;
+    double r = fma(-kd, ln2_hi, x);
+    r = fma(-kd, ln2_lo, r);
+    double p = 0x1.6124613a86d09p-33;                      /* 1/13! */
+    p = fma(p, r, 0x1.1eed8eff8d898p-29);                  /* 1/12! */
+    p = fma(p, r, 0x1.ae64567f544e4p-26);                  /* 1/11! */
+    p = fma(p, r, 0x1.27e4fb7789f5cp-22);                  /* 1/10! */
+    p = fma(p, r, 0x1.71de3a556c734p-19);                  /* 1/9!  */
+    p = fma(p, r, 0x1.a01a01a01a01ap-16);                  /* 1/8!  */
+    p = fma(p, r, 0x1.a01a01a01a01ap-13);                  /* 1/7!  */
+    p = fma(p, r, 0x1.6c16c16c16c17p-10);                  /* 1/6!  */
+    p = fma(p, r, 0x1.1111111111111p-7);                   /* 1/5!  */
+    p = fma(p, r, 0x1.5555555555555p-5);                   /* 1/4!  */
+    p = fma(p, r, 0x1.5555555555555p-3);                   /* 1/3!  */
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    int k1 = k / 2, k2 = k - k1;                           /* k in [-1075,1024] */
+    return (p * orc_pow2i(k1)) * orc_pow2i(k2);
+}
+
+/* ------------------------------------------------------- sin/cos(2*pi*u) */
+/* u finite with |4u| < 2^51; used for u in [0,1). */
+static inline void orc_sincos2pi(double u, double* s_out, double* c_out) {
+    double q = floor(fma(u, 4.0, 0.5));
+    double r = fma(q, -0.25, u);                           /* exact, r in [-1/8, 1/8] */
+    double r2 = r * r;
+    double S = -0x1.6fadb9f155744p-1;                      /* (2pi)^15/15!, alternating */
+    S = fma(S, r2, 0x1.e8f434d018d63p+1);
+    S = fma(S, r2, -0x1.e3074fde8871fp+3);
+    S = fma(S, r2, 0x1.50783487ee782p+5);
+    S = fma(S, r2, -0x1.32d2cce62bd86p+6);
+    S = fma(S, r2, 0x1.466bc6775aae2p+6);
+    S = fma(S, r2, -0x1.4abbce625be53p+5);
+    S = fma(S, r2, 0x1.921fb54442d18p+2);
+    double C = 0x1.20c62c2f2d7f5p-2;                       /* (2pi)^16/16! */
+    C = fma(C, r2, -0x1.b6e24f44b128fp+0);
+    C = fma(C, r2, 0x1.f9d38a3763cc3p+2);
+    C = fma(C, r2, -0x1.a6d1f2a204a8cp+4);
+    C = fma(C, r2, 0x1.e1f506891babbp+5);
+    C = fma(C, r2, -0x1.55d3c7e3cbffap+6);
+    C = fma(C, r2, 0x1.03c1f081b5ac4p+6);
+    C = fma(C, r2, -0x1.3bd3cc9be45dep+4);
+    C = fma(C, r2, 1.0);
+    double sn = r * S;
+    int qi = ((int)q) & 3;
+    double so, co;
+    switch (qi) {
+        case 0:  so = sn;  co = C;   break;
+        case 1:  so = C;   co = -sn; break;
+        case 2:  so = -sn; co = -C;  break;
+        default: so = -C;  co = sn;  break;
+    }
+    *s_out = so; *c_out = co;
+}
+
+/* Four standard normals from one Philox block (two Box-Muller pairs). */
+static inline void orc_normals4(const uint32_t w[4], double z[4]) {
+    for (int p = 0; p < 2; ++p) {
+        double u1 = orc_uniform32_open(w[2 * p]);
+        double u2 = orc_uniform32(w[2 * p + 1]);
+        double rad = sqrt(-2.0 * orc_log(u1));
+        double s, c;
+        orc_sincos2pi(u2, &s, &c);
+        z[2 * p] = rad * c;
+        z[2 * p + 1] = rad * s;
+    }
+}
+
+/* Julia-0.2 round(): nearest, ties away from zero (HMCDA.jl:104). */
+static inline double orc_round_away(double x) {
+    double t = trunc(x);
+    double fr = x - t;                                     /* exact */
+    if (fr >= 0.5) t += 1.0;
+    else if (fr <= -0.5) t -= 1.0;
+    return t;
+}
+
+#endif

@@ -1,0 +1,452 @@
+/*
+ * oracle/oracle.c -- TEST INFRASTRUCTURE ONLY.  CPU restatement of MCMC.jl's
+ * model x sampler x SerialMC hot path, used by tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg as the checker.  Never linked into, loaded by
+ * or called from the product (mcmc.jl_amd/).
+ *
+ * Parity status: the reference is Julia 0.2 and cannot run here (no Julia, an
+ * un-vendored ReverseDiffSource include at src/dsl/modelparser.jl:13); it holds
+ * no golden vectors.  This restatement is pinned by
+ *   - the Random123 Philox4x32-10 known-answer vectors (tests/golden/philox_kat.json),
+ *   - the reference's distributional test restated (KS statistic, test/test_dists.jl:7-47),
+ *   - the reference's finite-difference gradient test restated (test/dsl/helper_diff.jl:8-37),
+ *   - the README's HMC statistics (README.md:110-154),
+ * and is otherwise "parity unpinned" at the bit level against Julia.
+ *
+ * Each function names the reference lines it follows.  Arithmetic order is the
+ * build's specification: sums left to right over coordinates
+ * (order 0, lane-per-chain kernels) or per-lane partials + xor butterfly over 64
+ * lanes (order 1, wave-per-chain kernels).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+#include "detmath.h"
+
+#define ORC_MODEL_ISO 1
+#define ORC_MODEL_NORMAL 2
+#define ORC_MODEL_LOGISTIC 3
+#define ORC_MODEL_LINEAR 4
+
+#define ORC_RWM 1
+#define ORC_MALA 2
+#define ORC_HMC 3
+#define ORC_HMCDA 4
+
+typedef struct {
+    int32_t kind;
+    int32_t d;
+    double mu, sigma;
+    double prior_sigma, noise_sigma, link_sign;
+    int64_t n;
+    const double* X;      /* [n][d] */
+    const double* Y;      /* [n]    */
+    const double* scale;  /* [d] model.scale */
+} orc_model;
+
+typedef struct {
+    int32_t kind;
+    int32_t tuner;
+    double scale;
+    double drift_step;
+    int64_t n_leaps;
+    double leap_step;
+    double rate, len, shrinkage, t0, step;
+    int64_t adapt_step, max_step;
+    double target_path, target_rate;
+    int64_t max_leaps;
+} orc_sampler;
+
+/* per-chain state, arrays of length nchains (x: [d][nchains]) */
+typedef struct {
+    double* x;
+    double* lp;
+    double* t_step;
+    double* t_bar;
+    double* t_h;
+    int32_t* t_leaps;
+    int32_t* t_acc;
+    int32_t* t_prop;
+} orc_state;
+
+static const double ORC_LOG2PI = 0x1.d67f1c864beb5p+0;
+static const double ORC_TWOPI = 0x1.921fb54442d18p+2;
+
+/* ------------------------------------------------------------ reductions */
+/* order 1: lane l of a 64-lane wave owns coordinates 4*(l + 64k) + e, e = 0..3, k = 0,1,...;
+   each lane accumulates its coordinates in (k, e) order, then xor butterfly 32,16,...,1. */
+static double orc_butterfly(double p[64]) {
+    for (int off = 32; off >= 1; off >>= 1) {
+        double q[64];
+        for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ off];
+        memcpy(p, q, sizeof q);
+    }
+    return p[0];
+}
+
+static double orc_dot(const double* v, int d, int order) {
+    if (order == 0) {
+        double a = 0.0;
+        for (int j = 0; j < d; ++j) a = fma(v[j], v[j], a);
+        return a;
+    }
+    double p[64];
+    for (int l = 0; l < 64; ++l) {
+        double a = 0.0;
+        for (int j0 = 4 * l; j0 < d; j0 += 256)
+            for (int e = 0; e < 4 && j0 + e < d; ++e) a = fma(v[j0 + e], v[j0 + e], a);
+        p[l] = a;
+    }
+    return orc_butterfly(p);
+}
+
+static double orc_sum(const double* t, int d, int order) {
+    if (order == 0) {
+        double a = 0.0;
+        for (int j = 0; j < d; ++j) a = a + t[j];
+        return a;
+    }
+    double p[64];
+    for (int l = 0; l < 64; ++l) {
+        double a = 0.0;
+        for (int j0 = 4 * l; j0 < d; j0 += 256)
+            for (int e = 0; e < 4 && j0 + e < d; ++e) a = a + t[j0 + e];
+        p[l] = a;
+    }
+    return orc_butterfly(p);
+}
+
+/* ------------------------------------------------------------ models */
+/* Returns lp; writes the gradient into g (length d) when g != NULL; tmp: d doubles of scratch. */
+static double orc_eval(const orc_model* m, const double* x, double* g, double* tmp, int order) {
+    const int d = m->d;
+    if (m->kind == ORC_MODEL_ISO) {
+        /* model(v -> -dot(v,v), grad = v -> -2v)  README.md:60,63; test/test_syntax.jl:40-41 */
+        double lp = -orc_dot(x, d, order);
+        if (g)
+            for (int j = 0; j < d; ++j) g[j] = -2.0 * x[j];
+        return lp;
+    }
+    if (m->kind == ORC_MODEL_NORMAL) {
+        /* v ~ Normal(mu, sigma): LLAcc(0.) + sum(logpdf(...)) (AccumulatorDerivRules.jl:10-20,
+           modelparser.jl:48-51); gradient rule dx += (mu - x)/(sigma*sigma)*ds (MCMCDerivRules.jl:57) */
+        const double logsig = orc_log(m->sigma);
+        for (int j = 0; j < d; ++j) {
+            double z = (x[j] - m->mu) / m->sigma;
+            tmp[j] = -0.5 * (z * z + ORC_LOG2PI) - logsig;
+        }
+        double lp = orc_sum(tmp, d, order);
+        int oos = !isfinite(lp);
+        if (oos) lp = -INFINITY;                  /* OutOfSupportError -> (-Inf, zero(beta)), modelparser.jl:64-72 */
+        if (g) {
+            const double s2 = m->sigma * m->sigma;
+            for (int j = 0; j < d; ++j) g[j] = oos ? 0.0 : (m->mu - x[j]) / s2;
+        }
+        return lp;
+    }
+    return NAN;
+}
+
+/* normals of step `step` for chain `chain`: coordinate j <- block j/4, slot j%4 */
+static void orc_normals(uint64_t seed, uint32_t chain, uint32_t step, int d, double* z) {
+    for (int b = 0; 4 * b < d; ++b) {
+        uint32_t w[4];
+        double zz[4];
+        orc_block(seed, chain, step, (uint32_t)b, ORC_TAG_NORMAL, w);
+        orc_normals4(w, zz);
+        for (int e = 0; e < 4 && 4 * b + e < d; ++e) z[4 * b + e] = zz[e];
+    }
+}
+
+static double orc_accept_uniform(uint64_t seed, uint32_t chain, uint32_t step) {
+    uint32_t w[4];
+    orc_block(seed, chain, step, 0u, ORC_TAG_ACCEPT, w);
+    return orc_uniform53(w[0], w[1]);
+}
+
+/* i in r = (burnin+1):thinning:len ?  (SerialMC.jl:35, :49) */
+static int orc_kept(int64_t i_loc, int64_t burnin, int64_t thinning, int64_t len, int64_t* kk) {
+    if (i_loc <= burnin || i_loc > len) return 0;
+    int64_t off = i_loc - burnin - 1;
+    if (off % thinning) return 0;
+    *kk = off / thinning;
+    return 1;
+}
+
+/* adapt!(tune, tuner): rate = accepted/proposed; step *= 1/(1+exp(-11*(rate-target))) + 0.5
+   (MALA.jl:36-39, HMC.jl:165-169) */
+static double orc_tune_factor(int32_t acc, int32_t prop, double target) {
+    double rate = (double)acc / (double)prop;
+    return 1.0 / (1.0 + orc_exp(-11.0 * (rate - target))) + 0.5;
+}
+
+/* `ratio > 0 || ratio > log(rand())`, uniform drawn only when needed (RWM.jl:63, MALA.jl:108) */
+static int orc_mh_short_circuit(uint64_t seed, uint32_t chain, uint32_t step, double ratio) {
+    if (ratio > 0.0) return 1;
+    return ratio > orc_log(orc_accept_uniform(seed, chain, step));
+}
+
+/* nl leapfrogs (HMC.jl:219-228) from (x, mom, g); returns the final lp */
+static double orc_trajectory(const orc_model* m, double eps, int64_t nl, double* x, double* mom, double* g,
+                             double lp, double* tmp, int order) {
+    const int d = m->d;
+    for (int64_t l = 0; l < nl; ++l) {
+        for (int j = 0; j < d; ++j) mom[j] = mom[j] + (0.5 * g[j]) * eps;   /* n.m += 0.5*n.grad*ve */
+        for (int j = 0; j < d; ++j) x[j] = x[j] + eps * mom[j];              /* n.pars += ve * n.m   */
+        lp = orc_eval(m, x, g, tmp, order);                                   /* calc!(n, ll)         */
+        for (int j = 0; j < d; ++j) mom[j] = mom[j] + (0.5 * g[j]) * eps;   /* n.m += 0.5*n.grad*ve */
+    }
+    return lp;
+}
+
+/* ------------------------------------------------------------ one chain */
+/* `len` steps of SerialMC (SerialMC.jl:47-67) for chain c, sampler loop counter continuing from step0. */
+static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, uint32_t chain, int64_t c,
+                      int64_t C, int64_t step0, int64_t burnin, int64_t thinning, int64_t len, orc_state* st,
+                      double* samples, double* grads, uint8_t* acc_out, int order, double* buf) {
+    const int d = m->d;
+    double* x = buf;          /* state: pars */
+    double* g = x + d;        /* state: grad */
+    double* xp = g + d;       /* proposal    */
+    double* gp = xp + d;
+    double* mom = gp + d;
+    double* tmp = mom + d;
+    double* sc = tmp + d;     /* RWM scale = model.scale .* sampler.scale (RWM.jl:52) */
+    for (int j = 0; j < d; ++j) x[j] = st->x[(size_t)j * C + c];
+    for (int j = 0; j < d; ++j) sc[j] = m->scale ? m->scale[j] * s->scale : s->scale;
+    double lp = st->lp[c];
+    (void)orc_eval(m, x, g, tmp, order);     /* state grad (deterministic recompute of the stored one) */
+
+    const int tuned = s->tuner && (s->kind == ORC_MALA || s->kind == ORC_HMC);
+    double h = (s->kind == ORC_MALA && tuned) ? st->t_step[c] : s->drift_step;
+    double eps = ((s->kind == ORC_HMC && tuned) || s->kind == ORC_HMCDA) ? st->t_step[c] : s->leap_step;
+    int64_t nl_fixed = (s->kind == ORC_HMC && tuned) ? (int64_t)st->t_leaps[c] : s->n_leaps;
+    double eps_bar = s->kind == ORC_HMCDA ? st->t_bar[c] : 0.0;
+    double h_bar = s->kind == ORC_HMCDA ? st->t_h[c] : 0.0;
+    int32_t n_acc = tuned ? st->t_acc[c] : 0;
+    int32_t n_prop = tuned ? st->t_prop[c] : 0;
+    const double mu = orc_log(10.0);          /* HMCDA.jl:92: mu = log(10*leapStep) with leapStep = 1 */
+    const int64_t max_leaps = s->max_leaps > 0 ? s->max_leaps : ((int64_t)1 << 20);
+
+    for (int64_t t = 0; t < len; ++t) {
+        const int64_t i = step0 + t + 1;      /* the sampler's loop counter (HMC.jl:252 `for i in 1:Inf`) */
+        int acc = 0;
+        double p_da = 0.0;
+        if (s->kind == ORC_RWM) {
+            /* RWM.jl:58-71 */
+            orc_normals(seed, chain, (uint32_t)i, d, mom);
+            for (int j = 0; j < d; ++j) xp[j] = x[j] + mom[j] * sc[j];        /* pars + randn(d) .* scale */
+            double lpp = orc_eval(m, xp, NULL, tmp, order);
+            double ratio = lpp - lp;
+            acc = orc_mh_short_circuit(seed, chain, (uint32_t)i, ratio);
+            if (acc) {
+                memcpy(x, xp, sizeof(double) * d);
+                lp = lpp;
+            }
+        } else if (s->kind == ORC_MALA) {
+            /* MALA.jl:89-125 */
+            if (tuned) n_prop += 1;
+            const double half = h / 2.0;
+            const double sq = sqrt(h);
+            const double twoh = 2.0 * h;
+            const double L = orc_log(ORC_TWOPI * h) / 2.0;                   /* log(2*pi*driftStep)/2 */
+            orc_normals(seed, chain, (uint32_t)i, d, mom);
+            for (int j = 0; j < d; ++j) {
+                double pm = x[j] + half * g[j];                               /* parsMean */
+                xp[j] = pm + sq * mom[j];                                     /* proposedPars */
+                double e = pm - xp[j];
+                tmp[j] = (-(e * e)) / twoh - L;
+            }
+            double qf = orc_sum(tmp, d, order);                               /* probNewGivenOld */
+            double lpp = orc_eval(m, xp, gp, tmp, order);                     /* evalallg(proposedPars) */
+            for (int j = 0; j < d; ++j) {
+                double e = (xp[j] + half * gp[j]) - x[j];
+                tmp[j] = (-(e * e)) / twoh - L;
+            }
+            double qb = orc_sum(tmp, d, order);                               /* probOldGivenNew */
+            double ratio = ((lpp + qb) - lp) - qf;
+            acc = orc_mh_short_circuit(seed, chain, (uint32_t)i, ratio);
+            if (acc) {
+                memcpy(x, xp, sizeof(double) * d);
+                memcpy(g, gp, sizeof(double) * d);
+                lp = lpp;
+                if (tuned) n_acc += 1;
+            }
+        } else {
+            /* HMC.jl:252-299 / HMCDA.jl:97-142 */
+            const int da = s->kind == ORC_HMCDA;
+            if (!da && tuned) n_prop += 1;
+            orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* state0.m = randn(model.size) */
+            const double H0 = -lp + 0.5 * orc_dot(mom, d, order);             /* update!(state0) */
+            memcpy(xp, x, sizeof(double) * d);
+            memcpy(gp, g, sizeof(double) * d);
+            int64_t nl;
+            if (da) {
+                double r = orc_round_away(s->len / eps);                      /* round(len/leapStep) */
+                nl = r < 1.0 ? 1 : (r > (double)max_leaps ? max_leaps : (int64_t)r);
+            } else {
+                nl = nl_fixed;
+            }
+            double lpl = orc_trajectory(m, eps, nl, xp, mom, gp, lp, tmp, order);
+            const double H = -lpl + 0.5 * orc_dot(mom, d, order);
+            const double u = orc_accept_uniform(seed, chain, (uint32_t)i);
+            if (da) {
+                p_da = fmin(1.0, orc_exp(H0 - H));                            /* min(1, exp(H0-H)), NaN-ignoring */
+                acc = u < p_da;
+            } else {
+                acc = u < orc_exp(H0 - H);
+            }
+            if (acc) {
+                memcpy(x, xp, sizeof(double) * d);
+                memcpy(g, gp, sizeof(double) * d);
+                lp = lpl;
+                if (!da && tuned) n_acc += 1;
+            }
+        }
+        int64_t kk;
+        if (orc_kept(i - step0, burnin, thinning, len, &kk)) {
+            if (samples)
+                for (int j = 0; j < d; ++j) samples[((size_t)kk * d + j) * C + c] = x[j];
+            if (grads && s->kind != ORC_RWM)
+                for (int j = 0; j < d; ++j) grads[((size_t)kk * d + j) * C + c] = g[j];
+            if (acc_out) acc_out[(size_t)kk * C + c] = (uint8_t)acc;
+        }
+        /* adaptation, with the runner's burnin (`i <= runner.burnin`, MALA.jl:116, HMC.jl:293) */
+        if (s->kind == ORC_MALA && tuned && i <= burnin && (i % s->adapt_step) == 0) {
+            h = h * orc_tune_factor(n_acc, n_prop, s->target_rate);
+            n_acc = 0;
+            n_prop = 0;
+        } else if (s->kind == ORC_HMC && tuned && i <= burnin && (i % s->adapt_step) == 0) {
+            eps = eps * orc_tune_factor(n_acc, n_prop, s->target_rate);
+            double nlf = ceil(s->target_path / eps);                         /* min(maxStep, ceil(targetPath/leapStep)) */
+            if (nlf > (double)s->max_step) nlf = (double)s->max_step;
+            if (nlf > (double)max_leaps) nlf = (double)max_leaps;
+            nl_fixed = (int64_t)nlf;
+            n_acc = 0;
+            n_prop = 0;
+        } else if (s->kind == ORC_HMCDA) {
+            const double di = (double)i;
+            if (di < (double)burnin) {                                        /* HMCDA.jl:133-138 */
+                double eta = 1.0 / (di + s->t0);
+                h_bar = (1.0 - eta) * h_bar + eta * (s->rate - p_da);
+                eps = orc_exp(mu - (sqrt(di) * h_bar) / s->shrinkage);
+                eta = orc_exp(orc_log(di) * (-s->step));                      /* i^(-step) */
+                eps_bar = orc_exp((1.0 - eta) * orc_log(eps_bar) + eta * orc_log(eps));
+            } else {
+                eps = eps_bar;                                                /* HMCDA.jl:140 */
+            }
+        }
+    }
+    for (int j = 0; j < d; ++j) st->x[(size_t)j * C + c] = x[j];
+    st->lp[c] = lp;
+    if (tuned || s->kind == ORC_HMCDA) st->t_step[c] = (s->kind == ORC_MALA) ? h : eps;
+    if (s->kind == ORC_HMCDA) {
+        st->t_bar[c] = eps_bar;
+        st->t_h[c] = h_bar;
+    }
+    if (tuned) {
+        if (s->kind == ORC_HMC) st->t_leaps[c] = (int32_t)nl_fixed;
+        st->t_acc[c] = n_acc;
+        st->t_prop[c] = n_prop;
+    }
+}
+
+/* ------------------------------------------------------------ exported API (ctypes) */
+
+/* SamplerTask initialisation: lp = eval(x), tuner state defaults.  Returns the number of
+   chains whose start is out of support ("Initial values out of model support", RWM.jl:55). */
+int64_t orc_init(const orc_model* m, const orc_sampler* s, int64_t C, orc_state* st, int order) {
+    const int d = m->d;
+    int64_t bad = 0;
+    double* buf = (double*)malloc(sizeof(double) * 2 * (size_t)(d > 0 ? d : 1));
+    double* x = buf;
+    double* tmp = buf + d;
+    for (int64_t c = 0; c < C; ++c) {
+        for (int j = 0; j < d; ++j) x[j] = st->x[(size_t)j * C + c];
+        double lp = orc_eval(m, x, NULL, tmp, order);
+        st->lp[c] = lp;
+        if (!isfinite(lp)) bad++;
+        const int tuned = s->tuner && (s->kind == ORC_MALA || s->kind == ORC_HMC);
+        if (s->kind == ORC_MALA && tuned) st->t_step[c] = s->drift_step;
+        if (s->kind == ORC_HMC && tuned) { st->t_step[c] = s->leap_step; st->t_leaps[c] = (int32_t)s->n_leaps; }
+        if (s->kind == ORC_HMCDA) { st->t_step[c] = 1.0; st->t_bar[c] = 1.0; st->t_h[c] = 0.0; }
+        if (tuned) { st->t_acc[c] = 0; st->t_prop[c] = 0; }
+    }
+    free(buf);
+    return bad;
+}
+
+/* run_serialmc over chains [c_begin, c_end) of a batch of C (SerialMC.jl:37-85).
+   samples/grads: [nkept][d][C]; acc_out: [nkept][C] bytes.  nthreads > 1 uses OpenMP. */
+void orc_run(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t chain0, int64_t C,
+             int64_t c_begin, int64_t c_end, int64_t step0, int64_t burnin, int64_t thinning, int64_t len,
+             orc_state* st, double* samples, double* grads, uint8_t* acc_out, int order, int nthreads) {
+    const int d = m->d;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    {
+        double* buf = (double*)malloc(sizeof(double) * 7 * (size_t)d);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t c = c_begin; c < c_end; ++c)
+            orc_chain(m, s, seed, (uint32_t)(chain0 + c), c, C, step0, burnin, thinning, len, st, samples, grads,
+                      acc_out, order, buf);
+        free(buf);
+    }
+    (void)nthreads;
+}
+
+/* model.eval / evalallg on a batch x[d][C] */
+void orc_eval_batch(const orc_model* m, int64_t C, const double* xs, double* lp, double* grad, int order) {
+    const int d = m->d;
+    double* buf = (double*)malloc(sizeof(double) * 3 * (size_t)d);
+    for (int64_t c = 0; c < C; ++c) {
+        for (int j = 0; j < d; ++j) buf[j] = xs[(size_t)j * C + c];
+        lp[c] = orc_eval(m, buf, buf + d, buf + 2 * d, order);
+        if (grad)
+            for (int j = 0; j < d; ++j) grad[(size_t)j * C + c] = buf[d + j];
+    }
+    free(buf);
+}
+
+/* detmath probes (same op codes as mcmc_debug_detmath) */
+void orc_detmath(int op, int64_t n, const double* x, const double* y, double* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        double a = x[i], r = 0.0, sn, cs;
+        switch (op) {
+            case 0: r = orc_log(a); break;
+            case 1: r = orc_exp(a); break;
+            case 2: orc_sincos2pi(a, &sn, &cs); r = sn; break;
+            case 3: orc_sincos2pi(a, &sn, &cs); r = cs; break;
+            case 4: r = sqrt(a); break;
+            case 5: r = a / y[i]; break;
+            case 6: {
+                uint64_t packed = (uint64_t)a;
+                uint32_t ctr[4] = {(uint32_t)packed, (uint32_t)y[i], (uint32_t)(packed >> 32), ORC_TAG_NORMAL};
+                uint32_t key[2] = {0u, 0u}, w[4];
+                double z[4];
+                orc_philox4x32_10(ctr, key, w);
+                orc_normals4(w, z);
+                for (int k = 0; k < 4; ++k) out[4 * i + k] = z[k];
+                continue;
+            }
+            case 7: r = orc_round_away(a); break;
+            case 8: {
+                uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
+                uint32_t key[2] = {0u, 0u}, w[4];
+                orc_philox4x32_10(ctr, key, w);
+                r = orc_uniform53(w[0], w[1]);
+            } break;
+            default: r = 0.0;
+        }
+        out[i] = r;
+    }
+}
+
+void orc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+    for (int64_t i = 0; i < n; ++i) orc_philox4x32_10(ctr + 4 * i, key + 2 * i, out + 4 * i);
+}

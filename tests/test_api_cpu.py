@@ -1,0 +1,165 @@
+"""CPU tests of the host API and the C ABI boundary (no compute calls: there is no GPU here).
+
+Covers the reference's constructor @asserts (RWM.jl:29, MALA.jl:55, HMC.jl:60-61,
+HMCDA.jl:33-36, samplers.jl:40-42, SerialMC.jl:25-27), the MALA-without-gradient
+error (test/test_syntax.jl:75, README.md:224), the `*` composition (MCMC.jl:87-98),
+DSL parameter packing (test/dsl/unit_tests.jl:29-34), and that libmcmc_hip.so loads
+and exports every symbol include/mcmc_hip.h declares.
+"""
+import ctypes as ct
+import os
+import re
+
+import numpy as np
+import pytest
+
+import mcmchip as mc
+from mcmchip import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "mcmc_hip.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int)\s+(mcmc_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(_lib.EXPORTED_SYMBOLS) == syms
+    assert lib.mcmc_abi_version() == 1
+
+
+def test_struct_layouts_match_header():
+    # sizes of the C structs (LP64): checked against a compiled probe of the header
+    assert ct.sizeof(_lib.RunnerCfg) == 24
+    assert ct.sizeof(_lib.ModelDesc) == 4 + 4 + 8 + 8 + 8 + 5 * 8 + 8 + 8 + 8
+    assert ct.sizeof(_lib.SamplerCfg) == 4 + 4 + 8 + 8 + 8 + 8 + 5 * 8 + 4 + 4 + 8 + 8 + 8 + 8 + 8
+    assert ct.sizeof(_lib.Outputs) == 5 * 8 + 8 + 8 + 8 + 8
+
+
+def test_header_struct_sizes_compiled(tmp_path):
+    src = tmp_path / "probe.c"
+    src.write_text('#include "mcmc_hip.h"\n#include <stdio.h>\nint main(void){printf("%zu %zu %zu %zu\\n",'
+                   'sizeof(mcmc_model_desc),sizeof(mcmc_sampler_cfg),sizeof(mcmc_runner_cfg),sizeof(mcmc_outputs));'
+                   'return 0;}\n')
+    exe = tmp_path / "probe"
+    assert os.system(f"gcc -I{ROOT}/include {src} -o {exe}") == 0
+    out = os.popen(str(exe)).read().split()
+    assert [int(v) for v in out] == [ct.sizeof(_lib.ModelDesc), ct.sizeof(_lib.SamplerCfg),
+                                     ct.sizeof(_lib.RunnerCfg), ct.sizeof(_lib.Outputs)]
+
+
+def test_validation_mirrors_reference_asserts():
+    lib = _lib.load()
+
+    def sv(**kw):
+        c = _lib.SamplerCfg()
+        for k, v in kw.items():
+            setattr(c, k, v)
+        rc = lib.mcmc_sampler_validate(ct.byref(c))
+        return rc, lib.mcmc_last_error().decode()
+
+    assert sv(kind=1, scale=0.1)[0] == 0
+    assert sv(kind=1, scale=0.0) == (1, "scale should be > 0")
+    assert sv(kind=2, drift_step=-1.0) == (1, "MALA drift step should be > 0")
+    assert sv(kind=3, n_leaps=0, leap_step=0.1) == (1, "inner steps should be > 0")
+    assert sv(kind=3, n_leaps=2, leap_step=0.0) == (1, "inner steps scaling should be > 0")
+    rc, msg = sv(kind=4, rate=1.5, len=2.0, shrinkage=0.05, t0=10.0, step=0.75)
+    assert rc == 1 and msg.startswith("Target acceptance rate (1.5)")
+    rc, msg = sv(kind=4, rate=0.65, len=2.0, shrinkage=0.0, t0=10.0, step=0.75)
+    assert rc == 1 and "shrinkage parameter" in msg
+    rc, msg = sv(kind=2, drift_step=0.1, tuner=1, adapt_step=0, max_step=10, target_rate=0.5)
+    assert rc == 1 and msg.startswith("Adaptation step size (0)")
+
+    def rv(b, t, n):
+        c = _lib.RunnerCfg(b, t, n)
+        return lib.mcmc_runner_validate(ct.byref(c)), lib.mcmc_last_error().decode()
+
+    assert rv(100, 1, 1000)[0] == 0
+    assert rv(-1, 1, 10) == (1, "Burnin rounds (-1) should be >= 0")
+    assert rv(10, 1, 10) == (1, "Total MCMC length (10) should be > to burnin (10)")
+    assert rv(0, 0, 10) == (1, "Thinning (0) should be >= 1")
+
+
+def test_python_constructors_assert_like_reference():
+    with pytest.raises(AssertionError, match="scale should be > 0"):
+        mc.RWM(0.0)
+    with pytest.raises(AssertionError, match="MALA drift step should be > 0"):
+        mc.MALA(0.0)
+    with pytest.raises(AssertionError, match="inner steps should be > 0"):
+        mc.HMC(0, 0.1)
+    with pytest.raises(AssertionError, match="Target acceptance rate"):
+        mc.HMCDA(rate=1.0)
+    with pytest.raises(AssertionError, match="Target acceptance rate"):
+        mc.EmpMCTuner(1.5)
+    h = mc.HMC(0.75)
+    assert (h.nLeaps, h.leapStep) == (10, 0.75)                     # HMC(leapStep::Float64)
+    h = mc.HMC(3)
+    assert (h.nLeaps, h.leapStep) == (3, 0.1)                       # HMC(nLeaps::Int)
+    h = mc.HMC(2, 0.1)
+    assert (h.nLeaps, h.leapStep) == (2, 0.1)
+    t = mc.EmpMCTuner(0.7)
+    assert mc.MALA(t).tuner is t and mc.MALA(t).driftStep == 1.0  # MALA(s::MCMCTuner)
+    da = mc.HMCDA()
+    assert (da.rate, da.len, da.shrinkage, da.t0, da.step) == (0.65, 2.0, 0.05, 10.0, 0.75)
+
+
+def test_model_semantics():
+    m1 = mc.model(mc.IsoNormalDot(), init=np.ones(3))
+    assert not m1.has_gradient and m1.size == 3 and (m1.scale == 1).all()
+    m2 = mc.model(mc.IsoNormalDot(), grad=mc.IsoNormalDot.grad, init=np.ones(3))
+    assert m2.has_gradient
+    m = mc.model(mc.IsoNormalDot(), init=2.0, scale=0.5)             # scalar init/scale (likmodel.jl:112,115)
+    assert m.size == 1 and m.init[0] == 2.0 and m.scale[0] == 0.5
+    with pytest.raises(AssertionError, match="scale parameter size"):
+        mc.model(mc.IsoNormalDot(), init=np.ones(3), scale=np.ones(2))
+    # DSL packing: column-major, keyword order (expr_funcs.jl:76-90; test/dsl/unit_tests.jl:29-34)
+    m = mc.model(mc.NormalDSL(), a=1.0, b=np.array([2.0, 3.0]), c=np.array([[4.0, 5.0], [6.0, 7.0]]))
+    assert list(m.init) == [1.0, 2.0, 3.0, 4.0, 6.0, 5.0, 7.0]
+    with pytest.raises(AssertionError, match="'init' kwargs not allowed"):
+        mc.model(mc.NormalDSL(), init=np.ones(2), v=np.ones(2))
+
+
+def test_needs_gradient_error():
+    """run(mymodel3 * MALA(0.1) * SerialMC(1:1000)) throws (README.md:224, test_syntax.jl:75)."""
+    m3 = mc.model(mc.NormalDSL(0, 1), v=np.ones(3))
+    with pytest.raises(AssertionError, match="MALA sampler requires model with gradient function"):
+        m3 * mc.MALA(0.1) * mc.SerialMC(range(1, 1001))
+    with pytest.raises(AssertionError, match="HMC sampler requires model with gradient function"):
+        m3 * mc.HMC(2, 0.1) * mc.SerialMC(steps=10)
+    t = m3 * mc.RWM(0.1) * mc.SerialMC(steps=10)
+    assert isinstance(t, mc.MCMCTask)
+
+
+def test_star_composition_broadcasts():
+    m = mc.model(mc.IsoNormalDot(), grad=True, init=np.ones(3))
+    ts = m * [mc.RWM(0.1), mc.MALA(0.1), mc.HMC(3, 0.1)] * mc.SerialMC(steps=1000)
+    assert len(ts) == 3 and [type(t.sampler).__name__ for t in ts] == ["RWM", "MALA", "HMC"]
+    ts = m * [mc.HMC(i, 0.1) for i in range(1, 6)] * mc.SerialMC(steps=1000)
+    assert [t.sampler.nLeaps for t in ts] == [1, 2, 3, 4, 5]
+
+
+def test_no_gpu_means_loud_failure():
+    if mc.device_count() > 0:
+        pytest.skip("a GPU is present")
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(3))
+    with pytest.raises(mc.MCMCError):
+        mc.run(m * mc.RWM(0.1) * mc.SerialMC(steps=10))
+
+
+def test_accept_bit_unpacking():
+    from mcmchip.api import _unpack_bits
+    C = 130
+    rng = np.random.default_rng(0)
+    acc = rng.random((4, C)) < 0.5
+    words = np.zeros((4, 3), dtype=np.uint64)
+    for k in range(4):
+        for c in range(C):
+            if acc[k, c]:
+                words[k, c // 64] |= np.uint64(1) << np.uint64(c % 64)
+    assert np.array_equal(_unpack_bits(words, C), acc.T)

@@ -1,0 +1,211 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle on the same seeds.
+
+Bar (BASELINE.json north_star): samples within 1e-10 relative fp64 and accept
+bits bit-identical.  The build's arithmetic is specified operation by operation
+(DESIGN.md §3-4), so in practice samples are compared bit for bit; the 1e-10
+tolerance is the stated fallback and is asserted too.
+"""
+import numpy as np
+import pytest
+
+import mcmchip as mc
+from mcmchip import _lib
+import oracle_ref as orc
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-10
+
+
+def _ctx():
+    from mcmchip.api import _ctx
+    return _ctx(0)
+
+
+# ------------------------------------------------------------------ math layer
+def test_device_philox_known_answers(gpu):
+    import json, os, ctypes as ct
+    kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "philox_kat.json")))["vectors"]
+    ctr = np.array([[int(x, 16) for x in v["ctr"]] for v in kat], dtype=np.uint32)
+    key = np.array([[int(x, 16) for x in v["key"]] for v in kat], dtype=np.uint32)
+    out = np.zeros_like(ctr)
+    P = ct.POINTER(ct.c_uint32)
+    _lib.check(_lib.load().mcmc_debug_philox(_ctx(), len(ctr), ctr.ctypes.data_as(P), key.ctypes.data_as(P),
+                                              out.ctypes.data_as(P)))
+    assert [[format(int(x), "08x") for x in row] for row in out] == [v["out"] for v in kat]
+    rng = np.random.default_rng(1)
+    ctr = rng.integers(0, 2**32, size=(4096, 4), dtype=np.uint64).astype(np.uint32)
+    key = rng.integers(0, 2**32, size=(4096, 2), dtype=np.uint64).astype(np.uint32)
+    out = np.zeros_like(ctr)
+    _lib.check(_lib.load().mcmc_debug_philox(_ctx(), len(ctr), ctr.ctypes.data_as(P), key.ctypes.data_as(P),
+                                              out.ctypes.data_as(P)))
+    assert np.array_equal(out, orc.philox(ctr, key))
+
+
+def _dev_math(op, x, y=None):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float64)
+    out = np.empty(4 * len(x) if op == 6 else len(x))
+    _lib.check(_lib.load().mcmc_debug_detmath(_ctx(), op, len(x), _lib.dptr(x), _lib.dptr(y), _lib.dptr(out)))
+    return out
+
+
+@pytest.mark.parametrize("op,name", [(0, "log"), (1, "exp"), (2, "sin2pi"), (3, "cos2pi"), (4, "sqrt"),
+                                     (5, "div"), (7, "round")])
+def test_device_detmath_bitwise(gpu, op, name):
+    rng = np.random.default_rng(op)
+    if op == 0:
+        x = np.concatenate([np.exp(rng.uniform(-740, 709, 200000)), [0.0, -0.0, -1.0, np.inf, np.nan, 5e-324, 1.0]])
+    elif op == 1:
+        x = np.concatenate([rng.uniform(-750, 712, 200000), [0.0, np.inf, -np.inf, np.nan]])
+    elif op in (2, 3):
+        x = np.floor(rng.uniform(0, 2**32, 200000)) * 2.0**-32
+    elif op == 4:
+        x = np.exp(rng.uniform(-700, 700, 200000))
+    elif op == 5:
+        x = rng.normal(size=200000) * np.exp(rng.uniform(-300, 300, 200000))
+    else:
+        x = np.concatenate([rng.uniform(-1e6, 1e6, 100000), np.arange(-50, 50) + 0.5])
+    y = np.exp(rng.uniform(-300, 300, len(x))) if op == 5 else None
+    d, h = _dev_math(op, x, y), orc.detmath(op, x, y)
+    same = (d.view(np.uint64) == h.view(np.uint64)) | (np.isnan(d) & np.isnan(h))
+    assert same.all(), f"{name}: {np.count_nonzero(~same)} mismatches, e.g. x={x[~same][:3]}"
+
+
+def test_device_normals_bitwise(gpu):
+    n = 50000
+    a = np.arange(n, dtype=float) + 2.0**32 * 3
+    z, zh = _dev_math(6, a, np.full(n, 17.0)), orc.detmath(6, a, np.full(n, 17.0))
+    assert np.array_equal(z.view(np.uint64), zh.view(np.uint64))
+    u, uh = _dev_math(8, np.arange(n, dtype=float)), orc.detmath(8, np.arange(n, dtype=float))
+    assert np.array_equal(u, uh)
+
+
+# ------------------------------------------------------------------ samplers
+def _model(kind, d):
+    if kind == "iso":
+        return mc.model(mc.IsoNormalDot(), init=np.linspace(0.5, 1.5, d), grad=True,
+                        scale=np.linspace(0.8, 1.2, d))
+    return mc.model(mc.NormalDSL(0.3, 1.7), v=np.linspace(-1, 1, d), gradient=True)
+
+
+SAMPLERS = {
+    "rwm": lambda: mc.RWM(0.6),
+    "mala": lambda: mc.MALA(0.4),
+    "mala_tuned": lambda: mc.MALA(2.0, mc.EmpMCTuner(0.6, adaptStep=7)),
+    "hmc": lambda: mc.HMC(4, 0.3),
+    "hmc_tuned": lambda: mc.HMC(3, 0.9, mc.EmpMCTuner(0.7, adaptStep=5, maxStep=9)),
+    "hmcda": lambda: mc.HMCDA(len=0.8),
+}
+
+
+def assert_parity(chain, s_ref, g_ref, acc_ref, kind):
+    s = chain._samples
+    assert s.shape == s_ref.shape
+    acc = chain.diagnostics["accept"].T
+    assert np.array_equal(acc, acc_ref.astype(bool)), f"accept bits differ in {np.count_nonzero(acc != acc_ref)}"
+    np.testing.assert_allclose(s, s_ref, rtol=RTOL, atol=0)
+    assert np.array_equal(s.view(np.uint64), s_ref.view(np.uint64)), "samples not bit-identical"
+    if g_ref is not None and kind != "rwm":
+        np.testing.assert_allclose(chain._gradients, g_ref, rtol=RTOL, atol=0)
+
+
+@pytest.mark.parametrize("sname", list(SAMPLERS))
+@pytest.mark.parametrize("mkind", ["iso", "normal"])
+@pytest.mark.parametrize("d", [1, 3, 7, 16, 32])
+def test_sampler_parity(gpu, sname, mkind, d):
+    m = _model(mkind, d)
+    C = 200                                              # not a multiple of 64: tail wave
+    r = mc.SerialMC(steps=45, burnin=6, thinning=3)
+    task = m * SAMPLERS[sname]() * r
+    chain = mc.run(task, nchains=C, seed=12345 + d)
+    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=C, seed=12345 + d)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, sname)
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+
+
+@pytest.mark.parametrize("sname", ["rwm", "mala_tuned", "hmc_tuned", "hmcda"])
+def test_continue_run_matches_oracle(gpu, sname):
+    """run(chain) continues the same chains (runners.jl:14); tuners keep adapting only while i <= burnin."""
+    m = _model("normal", 5)
+    r = mc.SerialMC(steps=30, burnin=12, thinning=2)
+    task = (m * SAMPLERS[sname]() * r).batch(130, seed=77)
+    c1 = mc.run(task)
+    c2 = mc.run(c1)
+    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=130, seed=77)
+    s1, g1, a1 = oc.run(r)
+    s2, g2, a2 = oc.run(r)
+    assert_parity(c1, s1, g1, a1, sname)
+    assert_parity(c2, s2, g2, a2, sname)
+    assert task.steps_done == 60
+
+
+@pytest.mark.parametrize("spl", [1, 7])
+def test_steps_per_launch_is_invisible(gpu, spl):
+    m = _model("iso", 8)
+    r = mc.SerialMC(steps=40, burnin=5, thinning=4)
+    a = mc.run((m * mc.MALA(0.3) * r).batch(150, seed=3))
+    b = mc.run((m * mc.MALA(0.3) * r).batch(150, seed=3, steps_per_launch=spl))
+    assert np.array_equal(a._samples, b._samples)
+    assert np.array_equal(a.diagnostics["accept"], b.diagnostics["accept"])
+
+
+def test_chain_offset_sharding_is_invisible(gpu):
+    m = _model("iso", 4)
+    r = mc.SerialMC(steps=25, burnin=3)
+    full = mc.run((m * mc.HMC(3, 0.25) * r).batch(300, seed=5))
+    lo = mc.run((m * mc.HMC(3, 0.25) * r).batch(170, seed=5, chain_offset=0))
+    hi = mc.run((m * mc.HMC(3, 0.25) * r).batch(130, seed=5, chain_offset=170))
+    assert np.array_equal(np.concatenate([lo._samples, hi._samples], axis=2), full._samples)
+    assert np.array_equal(np.concatenate([lo.diagnostics["accept"], hi.diagnostics["accept"]]),
+                          full.diagnostics["accept"])
+
+
+def test_single_chain_readme_example(gpu):
+    """README.md:85: run(mymodel1, RWM(0.1), SerialMC(steps=1000, burnin=100)) -> 900 samples."""
+    m1 = mc.model(mc.IsoNormalDot(), init=np.ones(3))
+    ch = mc.run(m1, mc.RWM(0.1), mc.SerialMC(steps=1000, burnin=100))
+    assert ch.samples.shape == (1, 900, 3) and np.isnan(ch.gradients).all()
+    oc = orc.OracleChains(m1, mc.RWM(0.1), nchains=1, seed=1)
+    s, _, acc = oc.run(mc.SerialMC(steps=1000, burnin=100))
+    assert np.array_equal(ch._samples, s) and np.array_equal(ch.diagnostics["accept"].T, acc.astype(bool))
+    assert ch.diagnostics["step"] == list(range(101, 1001))
+    rate = mc.acceptance(ch)[0]
+    assert rate == 100 * acc.mean()
+
+
+def test_resume_restarts_from_init(gpu):
+    m = _model("iso", 3)
+    ch = mc.run((m * mc.RWM(0.5) * mc.SerialMC(steps=20, thinning=2)).batch(64, seed=9))
+    ch2 = mc.resume(ch, steps=30)
+    assert ch2.samples.shape == (64, 15, 3) and ch2.task.steps_done == 30
+
+
+def test_model_eval_matches_oracle(gpu):
+    for kind in ("iso", "normal"):
+        m = _model(kind, 9)
+        x = np.random.default_rng(0).normal(size=(9, 333)) * 3
+        lp, g = m.evalallg(x)
+        lp_r, g_r = orc.eval_batch(m, x)
+        assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
+
+
+def test_init_out_of_support(gpu):
+    m = mc.model(mc.NormalDSL(0, 1), v=np.zeros(2), gradient=True)
+    bad = np.array([[np.inf, 0.0, 0.0], [0.0, 0.0, 0.0]])
+    with pytest.raises(mc.OutOfSupportError, match="Initial values out of model support"):
+        mc.run((m * mc.RWM(0.1) * mc.SerialMC(steps=5)).batch(3, init_x=bad))
+    with pytest.raises(mc.OutOfSupportError):
+        mc.model(mc.NormalDSL(0, 1), v=np.array([np.inf]), gradient=True)._handle(0)
+
+
+def test_divergent_hmc_rejects(gpu):
+    """Huge leapfrog steps on the DSL target: out-of-support trajectories (-Inf, zero grad) must reject."""
+    m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.ones(4), gradient=True)
+    r = mc.SerialMC(steps=20)
+    ch = mc.run((m * mc.HMC(30, 1e150) * r).batch(70, seed=4))
+    oc = orc.OracleChains(m, mc.HMC(30, 1e150), nchains=70, seed=4)
+    s, g, acc = oc.run(r)
+    assert_parity(ch, s, g, acc, "hmc")
+    assert not ch.diagnostics["accept"].any()

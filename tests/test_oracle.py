@@ -1,0 +1,272 @@
+"""CPU tests of the oracle (oracle/oracle.c) -- pins the parity checker.
+
+The reference ships no golden vectors; the oracle is pinned by
+  * the Random123 Philox4x32-10 known-answer vectors,
+  * a numpy twin of the stream (independent restatement),
+  * accuracy of the deterministic fp64 math against numpy/libm,
+  * the reference's own distributional test (KS, test/test_dists.jl:7-47),
+  * the reference's finite-difference gradient test (test/dsl/helper_diff.jl:8-37),
+  * the README's HMC statistics (README.md:110-154),
+  * bookkeeping invariants (SerialMC ranges, continuation, sharding).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+from scipy import stats
+
+import mcmchip as mc
+import oracle_ref as orc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ------------------------------------------------------------------ Philox
+def _kat():
+    with open(os.path.join(HERE, "golden", "philox_kat.json")) as f:
+        return json.load(f)["vectors"]
+
+
+def test_philox_known_answers():
+    for v in _kat():
+        ctr = np.array([int(x, 16) for x in v["ctr"]], dtype=np.uint32)
+        key = np.array([int(x, 16) for x in v["key"]], dtype=np.uint32)
+        out = orc.philox(ctr, key)[0]
+        assert [format(int(x), "08x") for x in out] == v["out"]
+
+
+def philox_numpy(ctr, key):
+    """Independent numpy restatement of Philox4x32-10 (Salmon et al. 2011)."""
+    c = [ctr[:, i].astype(np.uint64) for i in range(4)]
+    k0, k1 = key[:, 0].astype(np.uint64), key[:, 1].astype(np.uint64)
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    mask = np.uint64(0xFFFFFFFF)
+    for r in range(10):
+        if r:
+            k0 = (k0 + np.uint64(0x9E3779B9)) & mask
+            k1 = (k1 + np.uint64(0xBB67AE85)) & mask
+        p0 = M0 * c[0]
+        p1 = M1 * c[2]
+        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k0) & mask, p1 & mask, ((p0 >> np.uint64(32)) ^ c[3] ^ k1) & mask,
+             p0 & mask]
+    return np.stack(c, axis=1).astype(np.uint32)
+
+
+def test_philox_matches_numpy_twin():
+    rng = np.random.default_rng(7)
+    ctr = rng.integers(0, 2**32, size=(5000, 4), dtype=np.uint64).astype(np.uint32)
+    key = rng.integers(0, 2**32, size=(5000, 2), dtype=np.uint64).astype(np.uint32)
+    assert np.array_equal(orc.philox(ctr, key), philox_numpy(ctr, key))
+
+
+# ------------------------------------------------------------------ deterministic math
+def _ulps(a, b):
+    return np.abs(a - b) / np.spacing(np.maximum(np.abs(b), np.finfo(float).tiny))
+
+
+def test_det_log_accuracy():
+    rng = np.random.default_rng(0)
+    for lo, hi in [(1e-300, 1e-200), (0.3, 3.0), (2.0, 1e10), (1e-320, 1e-310)]:
+        x = rng.uniform(lo, hi, 100000)
+        assert _ulps(orc.detmath(0, x), np.log(x)).max() <= 1.0
+    sp = orc.detmath(0, np.array([0.0, -0.0, -1.0, np.inf, np.nan, 1.0]))
+    assert sp[0] == -np.inf and sp[1] == -np.inf and np.isnan(sp[2]) and sp[3] == np.inf and np.isnan(sp[4])
+    assert sp[5] == 0.0
+
+
+def test_det_exp_accuracy():
+    rng = np.random.default_rng(1)
+    x = rng.uniform(-700, 700, 100000)
+    assert _ulps(orc.detmath(1, x), np.exp(x)).max() <= 1.0
+    sp = orc.detmath(1, np.array([0.0, -1000.0, 1000.0, np.nan, -np.inf, np.inf]))
+    assert sp[0] == 1.0 and sp[1] == 0.0 and sp[2] == np.inf and np.isnan(sp[3]) and sp[4] == 0 and sp[5] == np.inf
+
+
+def test_det_sincos2pi_accuracy():
+    rng = np.random.default_rng(2)
+    u = np.floor(rng.uniform(0, 2**32, 100000)) * 2.0**-32
+    s, c = orc.detmath(2, u), orc.detmath(3, u)
+    assert np.abs(s - np.sin(2 * np.pi * u)).max() < 2e-15
+    assert np.abs(c - np.cos(2 * np.pi * u)).max() < 2e-15
+    q = orc.detmath(2, np.array([0.0, 0.25, 0.5, 0.75]))
+    assert np.allclose(q, [0, 1, 0, -1], atol=1e-16)
+
+
+def test_round_ties_away_from_zero():
+    x = np.array([0.5, 1.5, 2.5, -0.5, -2.5, 2.4999999999, 0.49999999999999994, 3.0])
+    assert list(orc.detmath(7, x)) == [1, 2, 3, -1, -3, 2, 0, 3]      # Julia 0.2 round (HMCDA.jl:104)
+
+
+def test_normals_are_standard_normal():
+    n = 50000
+    z = orc.detmath(6, np.arange(n, dtype=float), np.full(n, 3.0)).reshape(-1)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    assert stats.kstest(z, "norm").pvalue > 1e-3
+    # 32-bit Box-Muller radius bound: sqrt(-2 log(2^-33)) = 6.76
+    assert np.abs(z).max() < 6.77
+
+
+def test_uniform53_range():
+    u = orc.detmath(8, np.arange(20000, dtype=float))
+    assert u.min() >= 0.0 and u.max() < 1.0
+    assert stats.kstest(u, "uniform").pvalue > 1e-3
+
+
+# ------------------------------------------------------------------ models
+@pytest.mark.parametrize("mk", ["iso", "normal"])
+def test_gradient_finite_difference(mk):
+    """helper_diff.jl:8-37: DIFF_DELTA = 1e-9, relative error threshold 2e-2."""
+    d = 5
+    m = (mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True) if mk == "iso"
+         else mc.model(mc.NormalDSL(1.0, 2.0), v=np.ones(d), gradient=True))
+    rng = np.random.default_rng(3)
+    x0 = rng.normal(size=(d, 4))
+    lp0, g0 = orc.eval_batch(m, x0)
+    delta = 1e-9
+    for j in range(d):
+        x1 = x0.copy()
+        x1[j] += delta
+        lp1, _ = orc.eval_batch(m, x1)
+        gn = (lp1 - lp0) / delta
+        err = np.abs(g0[j] - gn) / np.maximum(2e-2, np.abs(g0[j]))
+        assert (err < 2e-2).all()
+
+
+def test_normal_dsl_logpdf_and_out_of_support():
+    m = mc.model(mc.NormalDSL(1.0, 2.0), v=np.zeros(3), gradient=True)
+    x = np.array([[0.3], [-1.0], [2.5]])
+    lp, g = orc.eval_batch(m, x)
+    assert np.isclose(lp[0], stats.norm(1, 2).logpdf(x[:, 0]).sum(), rtol=1e-14)
+    assert np.allclose(g[:, 0], (1.0 - x[:, 0]) / 4.0, rtol=1e-15)
+    # LLAcc: a non-finite running sum -> (-Inf, zeros) (AccumulatorDerivRules.jl:14-16, modelparser.jl:68)
+    lp, g = orc.eval_batch(m, np.array([[np.inf], [0.0], [0.0]]))
+    assert lp[0] == -np.inf and (g == 0).all()
+
+
+# ------------------------------------------------------------------ samplers: statistics
+def _pool(samples, every=1):
+    return samples[::every].reshape(-1)
+
+
+@pytest.mark.parametrize("mu,sd", [(1.0, 1.0), (3.0, 12.0)])
+@pytest.mark.parametrize("which", ["RWM", "HMC", "MALA"])
+def test_ks_like_reference(mu, sd, which):
+    """test_dists.jl:24-47: RWM(std), HMC(2, std/5), MALA(std) on x ~ Normal(mu, sd), SerialMC(1000:N),
+    KS measure below the reference's threshold 10; here over 64 chains, one kept sample per chain and
+    per 50 steps, against the 5 % critical value."""
+    sampler = {"RWM": mc.RWM(sd), "HMC": mc.HMC(2, sd / 5), "MALA": mc.MALA(sd)}[which]
+    m = mc.model(mc.NormalDSL(mu, sd), x=mu, gradient=True)
+    oc = orc.OracleChains(m, sampler, nchains=64, seed=11)
+    r = mc.SerialMC(range(1000, 6001))
+    s, _, _ = oc.run(r)
+    x = s[::50, 0, :].reshape(-1)                         # 101 x 64 draws, nearly independent
+    xs = np.sort(x)
+    dn = np.max(np.abs(np.arange(1, len(x) + 1) / len(x) - stats.norm(mu, sd).cdf(xs)))
+    ksv = math.sqrt(len(x)) * dn
+    assert ksv < 10.0                                      # the reference's KSTHRESHOLD (test_dists.jl:13)
+    assert ksv < 2.5                                       # and a meaningful bound
+
+
+def test_readme_hmc_statistics():
+    """README.md:110-154: HMC(0.75) on -dot(v,v), d=3, SerialMC(steps=10000, burnin=1000): acceptance 79.76 %,
+    AC time 1.687 -- the reference's numbers come from one dSFMT chain; here the mean over 16 Philox chains."""
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(3), grad=True)
+    oc = orc.OracleChains(m, mc.HMC(0.75), nchains=16, seed=5)
+    r = mc.SerialMC(steps=10000, burnin=1000)
+    s, _, acc = oc.run(r)
+    rate = acc.mean() * 100
+    assert abs(rate - 79.76) < 1.5
+    chain = type("C", (), {})()
+    chain.samples = np.transpose(s, (2, 0, 1))
+    act = mc.actime(chain)
+    assert abs(act.mean() - 1.687) < 0.15
+    assert np.allclose(s.reshape(-1, 3 * 16).std(axis=0), math.sqrt(0.5), atol=0.05)   # N(0, I/2)
+
+
+def test_hmcda_adapts_towards_target_rate():
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(8), grad=True)
+    oc = orc.OracleChains(m, mc.HMCDA(rate=0.65, len=1.0), nchains=32, seed=2)
+    _, _, acc = oc.run(mc.SerialMC(steps=3000, burnin=1000))
+    assert abs(acc.mean() - 0.65) < 0.1
+    assert (oc.t_step == oc.t_bar).all()                    # after burn-in leapStep = dualLeapStep
+
+
+def test_tuned_mala_and_hmc_adapt():
+    m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.zeros(4), gradient=True)
+    oc = orc.OracleChains(m, mc.MALA(5.0, mc.EmpMCTuner(0.6, adaptStep=50)), nchains=16, seed=3)
+    _, _, acc = oc.run(mc.SerialMC(steps=2000, burnin=1000))
+    assert abs(acc.mean() - 0.6) < 0.15
+    assert (oc.t_step != 5.0).all()
+    oc = orc.OracleChains(m, mc.HMC(10, 2.0, mc.EmpMCTuner(0.7, adaptStep=50, maxStep=40)), nchains=16, seed=3)
+    _, _, acc = oc.run(mc.SerialMC(steps=2000, burnin=1000))
+    assert (oc.t_leaps <= 40).all() and (oc.t_leaps >= 1).all()
+
+
+# ------------------------------------------------------------------ bookkeeping invariants
+def test_serialmc_ranges():
+    r = mc.SerialMC(steps=1000, burnin=100)
+    assert (r.burnin, r.thinning, r.len, len(r.r)) == (100, 1, 1000, 900)
+    r = mc.SerialMC(steps=1000, burnin=100, thinning=5)
+    assert len(r.r) == 180 and r.r[0] == 101
+    r = mc.SerialMC(range(101, 1001, 5))                    # SerialMC(101:5:1000)
+    assert (r.burnin, r.thinning, r.len, len(r.r)) == (100, 5, 996, 180)
+    with pytest.raises(AssertionError, match="Burnin rounds"):
+        mc.SerialMC(steps=10, burnin=-1)
+    with pytest.raises(AssertionError, match="Total MCMC length"):
+        mc.SerialMC(steps=10, burnin=10)
+    with pytest.raises(AssertionError, match="Thinning"):
+        mc.SerialMC(steps=10, thinning=0)
+
+
+def test_kept_steps_store_post_step_state():
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(3))
+    oc = orc.OracleChains(m, mc.RWM(0.5), nchains=5, seed=4)
+    s_all, _, a_all = oc.run(mc.SerialMC(steps=30))
+    oc2 = orc.OracleChains(m, mc.RWM(0.5), nchains=5, seed=4)
+    s_thin, _, a_thin = oc2.run(mc.SerialMC(steps=30, burnin=4, thinning=7))
+    idx = np.arange(4, 30, 7)                                  # kept steps 5, 12, 19, 26 (1-based)
+    assert np.array_equal(s_thin, s_all[idx]) and np.array_equal(a_thin, a_all[idx])
+    assert np.array_equal(oc.x, oc2.x)
+
+
+def test_continuation_equals_one_long_run():
+    """run(chain) continues the same Markov chain (runners.jl:14): the counter-based stream makes
+    two runs of 40 steps bit-identical to the last 40 of one 80-step run."""
+    m = mc.model(mc.NormalDSL(0.5, 1.5), v=np.zeros(6), gradient=True)
+    for sp in (mc.RWM(0.7), mc.MALA(0.3), mc.HMC(4, 0.3), mc.HMCDA(len=1.0)):
+        a = orc.OracleChains(m, sp, nchains=7, seed=9)
+        a.run(mc.SerialMC(steps=40, burnin=0))
+        s2, _, acc2 = a.run(mc.SerialMC(steps=40, burnin=0))
+        b = orc.OracleChains(m, sp, nchains=7, seed=9)
+        s, _, acc = b.run(mc.SerialMC(steps=80, burnin=0))
+        assert np.array_equal(s2, s[40:]) and np.array_equal(acc2, acc[40:])
+
+
+def test_sharding_is_invisible():
+    """Chains keyed by global id: two shards with chain_offset reproduce one batch."""
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(4), grad=True)
+    full = orc.OracleChains(m, mc.HMC(3, 0.2), nchains=10, seed=8)
+    s, _, acc = full.run(mc.SerialMC(steps=25, burnin=5))
+    lo = orc.OracleChains(m, mc.HMC(3, 0.2), nchains=6, seed=8, chain_offset=0)
+    hi = orc.OracleChains(m, mc.HMC(3, 0.2), nchains=4, seed=8, chain_offset=6)
+    s_lo, _, a_lo = lo.run(mc.SerialMC(steps=25, burnin=5))
+    s_hi, _, a_hi = hi.run(mc.SerialMC(steps=25, burnin=5))
+    assert np.array_equal(np.concatenate([s_lo, s_hi], axis=2), s)
+    assert np.array_equal(np.concatenate([a_lo, a_hi], axis=1), acc)
+
+
+def test_wave_order_reduction_is_a_sum():
+    """order 1 (wave-per-chain kernels) changes only the summation order."""
+    m = mc.model(mc.NormalDSL(0.2, 1.3), v=np.zeros(300), gradient=True)
+    x = np.random.default_rng(5).normal(size=(300, 3))
+    lp0, g0 = orc.eval_batch(m, x, order=0)
+    lp1, g1 = orc.eval_batch(m, x, order=1)
+    assert np.allclose(lp0, lp1, rtol=1e-13) and np.array_equal(g0, g1)
+
+
+def test_init_out_of_support_raises():
+    m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.zeros(2), gradient=True)
+    with pytest.raises(AssertionError, match="out of model support"):
+        orc.OracleChains(m, mc.RWM(0.1), nchains=2, init_x=np.array([[np.inf, 0.0], [0.0, 0.0]]))
