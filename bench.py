@@ -30,16 +30,30 @@ sys.path.insert(0, os.path.join(ROOT, "mcmc.jl_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+# BASELINE.json configs (per-GPU chain counts for the sharded ones)
+CONFIGS = {
+    "metric": dict(d=32, chains=1 << 20, sampler="rwm", thinning=10,
+                   desc="d=32 iso-Normal, RWM(0.1), 2^20 chains/GPU (BASELINE metric)"),
+    "readme": dict(d=3, chains=1, sampler="rwm", thinning=1,
+                   desc="config 1: d=3 iso-Normal, RWM(0.1), SerialMC(1000,100), 1 chain"),
+    "d3": dict(d=3, chains=1 << 20, sampler="rwm", thinning=10,
+               desc="config 2: d=3 iso-Normal, RWM(0.1), 1,048,576 chains"),
+    "hmc1024": dict(d=1024, chains=524288 // 8, sampler="hmc", thinning=100,
+                    desc="config 4: d=1024 iso-Normal, HMC(10, 0.1), 524,288 chains over 8 GPUs (65,536/GPU)"),
+}
+
 
 def parse():
     p = argparse.ArgumentParser()
+    p.add_argument("--config", default="metric", choices=list(CONFIGS),
+                   help="BASELINE.json workload (metric = 2^20 chains x d=32 RWM)")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--d", type=int, default=32)
-    p.add_argument("--chains", type=int, default=1 << 20, help="chains per GPU")
-    p.add_argument("--sampler", default="rwm", choices=["rwm", "mala", "hmc", "hmcda"])
-    p.add_argument("--thinning", type=int, default=10)
+    p.add_argument("--d", type=int, default=None)
+    p.add_argument("--chains", type=int, default=None, help="chains per GPU")
+    p.add_argument("--sampler", default=None, choices=["rwm", "mala", "hmc", "hmcda"])
+    p.add_argument("--thinning", type=int, default=None)
     p.add_argument("--spl", type=int, default=-1, help="steps per launch (0: whole run in one launch; "
                                                        "-1: default of the library)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,8 +110,12 @@ def main():
     import mcmchip as mc
     from mcmchip import _lib
 
+    cfg0 = CONFIGS[args.config]
+    for k in ("d", "chains", "sampler", "thinning"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg0[k])
     d = args.d
-    C = args.chains // world if args.strong else args.chains
+    C = max(1, args.chains // world) if args.strong else args.chains
     model = mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
     sampler = {"rwm": lambda: mc.RWM(0.1), "mala": lambda: mc.MALA(0.1), "hmc": lambda: mc.HMC(10, 0.1),
                "hmcda": lambda: mc.HMCDA()}[args.sampler]()
@@ -165,7 +183,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic (model init ones(d); Philox4x32-10 stream, seed 1)",
         "config": {
-            "workload": f"iso-Normal -dot(v,v) d={d}, {type(sampler).__name__}, "
+            "workload": f"{args.config}: iso-Normal -dot(v,v) d={d}, {type(sampler).__name__}, "
                         f"SerialMC(steps={K}, burnin={burnin}, thinning={args.thinning}), {C} chains/GPU",
             "d": d, "chains_per_gpu": C, "global_chains": total_chains, "sampler": args.sampler,
             "burnin": burnin, "thinning": args.thinning, "kept_per_chain": nkept,
@@ -174,7 +192,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": f"lpc_{args.sampler}", "launches": launches, "avg_launch_ms": avg_launch_s * 1e3,
+            "kernel": f"{'lpc' if d <= 32 else 'wpc'}_{args.sampler}", "launches": launches, "avg_launch_ms": avg_launch_s * 1e3,
             "algorithmic_bytes_per_launch": nbytes / launches,
         },
     }

@@ -6,7 +6,7 @@
 #include "../common.hpp"
 
 namespace mcmc {
-struct LpcArgs {
+struct KernelArgs {
     StepArgs s;
     SamplerArgs sa;
     ModelArgs m;
@@ -14,15 +14,24 @@ struct LpcArgs {
 };
 }  // namespace mcmc
 
-hipError_t mcmc_launch_lpc_step(const mcmc::LpcArgs& a, hipStream_t st);
-hipError_t mcmc_launch_lpc_eval(const mcmc::LpcArgs& a, const double* xin, int64_t ldin, double* lp, double* g,
-                                int check, hipStream_t st);
+// lane-per-chain kernels (d <= 32), state [d][ld]
+hipError_t mcmc_launch_lpc_step(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_launch_lpc_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
+                                hipStream_t st);
 int mcmc_lpc_max_d();
+// wave-per-chain kernels (32 < d <= 4096), state [C][ld] (ld = row stride, multiple of 4)
+hipError_t mcmc_launch_wpc_step(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
+                                hipStream_t st);
+int mcmc_wpc_max_d();
 
 hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st);
 hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st);
 hipError_t mcmc_broadcast_cols(double* dst, int64_t ldd, const double* v, int d, int64_t C, hipStream_t st);
+hipError_t mcmc_broadcast_rows(double* dst, int64_t ldr, const double* v, int d, int64_t C, hipStream_t st);
 hipError_t mcmc_copy_cols(double* dst, int64_t ldd, const double* src, int64_t lds, int d, int64_t C, hipStream_t st);
-hipError_t mcmc_transpose(double* dst, const double* src, int64_t batch, int64_t R, int64_t S, hipStream_t st);
+// dst[b][s][r] (row stride ldd) <- src[b][r][s] (row stride lds), r < R, s < S; batch strides R*lds / S*ldd
+hipError_t mcmc_transpose(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t batch, int64_t R,
+                          int64_t S, hipStream_t st);
 hipError_t mcmc_detmath(int op, int64_t n, const double* x, const double* y, double* out, hipStream_t st);
 hipError_t mcmc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out, hipStream_t st);

@@ -81,11 +81,11 @@ struct mcmc_chains {
     Layout layout = LAYOUT_LPC;
     ChainState st{};
     double* d_scale_eff = nullptr;   // model.scale .* sampler.scale (RWM.jl:52)
-    double* d_init_x = nullptr;      // optional per-chain start, state layout
+    double* d_init_x = nullptr;      // optional per-chain start, [d][C]
     int64_t steps_done = 0;
     int64_t spl = 0;                 // steps per launch (0: whole run)
     int store_grads = 1;
-    DevBuf out_samples, out_grads, out_bits, out_tmp;
+    DevBuf out_samples, out_grads, out_bits, out_tmp, stage_samples, stage_grads;
 };
 
 static int set_device(mcmc_ctx* ctx) {
@@ -324,8 +324,14 @@ static bool model_is_separable(const mcmc_model* m) {
 
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
-static LpcArgs base_args(const mcmc_model* m, int64_t C, int64_t ld) {
-    LpcArgs a{};
+// State layout of a chain batch: lane-per-chain [d][ld] for d <= 32, wave-per-chain [C][ld] above.
+static Layout layout_for(const mcmc_model* m) {
+    return m->args.d <= mcmc_lpc_max_d() ? LAYOUT_LPC : LAYOUT_WPC;
+}
+static int64_t ld_for(Layout L, int64_t C, int d) { return L == LAYOUT_LPC ? round_up(C, 64) : round_up(d, 4); }
+
+static KernelArgs base_args(const mcmc_model* m, int64_t C, int64_t ld) {
+    KernelArgs a{};
     a.m = m->args;
     a.s.C = C;
     a.s.ld = ld;
@@ -335,6 +341,30 @@ static LpcArgs base_args(const mcmc_model* m, int64_t C, int64_t ld) {
     return a;
 }
 
+static hipError_t launch_eval(Layout L, const KernelArgs& a, const double* xin, double* lp, double* g, int check,
+                              hipStream_t st) {
+    return L == LAYOUT_LPC ? mcmc_launch_lpc_eval(a, xin, lp, g, check, st)
+                           : mcmc_launch_wpc_eval(a, xin, lp, g, check, st);
+}
+static hipError_t launch_step(Layout L, const KernelArgs& a, hipStream_t st) {
+    return L == LAYOUT_LPC ? mcmc_launch_lpc_step(a, st) : mcmc_launch_wpc_step(a, st);
+}
+
+// [d][C] (stride ldc) <-> state layout
+static hipError_t cols_to_state(Layout L, double* state, int64_t ld, const double* cols, int64_t ldc, int d, int64_t C,
+                                hipStream_t st) {
+    if (L == LAYOUT_LPC) return mcmc_copy_cols(state, ld, cols, ldc, d, C, st);
+    // [d][C] -> [C][ld]: transpose of a d x C matrix
+    hipError_t e = hipMemsetAsync(state, 0, (size_t)C * ld * 8, st);
+    if (e != hipSuccess) return e;
+    return mcmc_transpose(state, ld, cols, ldc, 1, d, C, st);
+}
+static hipError_t state_to_cols(Layout L, double* cols, int64_t ldc, const double* state, int64_t ld, int d, int64_t C,
+                                hipStream_t st) {
+    if (L == LAYOUT_LPC) return mcmc_copy_cols(cols, ldc, state, ld, d, C, st);
+    return mcmc_transpose(cols, ldc, state, ld, 1, C, d, st);
+}
+
 extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, double* lp, double* grad) {
     if (!m || !x || !lp) return fail(MCMC_E_INVALID_ARG, "NULL argument");
     if (nchains <= 0) return fail(MCMC_E_INVALID_ARG, "nchains should be > 0");
@@ -342,21 +372,31 @@ extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, 
     if (int r = set_device(ctx)) return r;
     const int d = m->args.d;
     if (!model_is_separable(m)) return fail(MCMC_E_UNSUPPORTED, "model kind has no eval kernel");
-    if (d > mcmc_lpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "eval for d > 32 is served by the wave-per-chain path");
-    double *dx = nullptr, *dlp = nullptr, *dg = nullptr;
+    if (d > mcmc_wpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "d > 2048 is not built");
+    const Layout L = layout_for(m);
+    const int64_t ld = ld_for(L, nchains, d);
+    const size_t nst = L == LAYOUT_LPC ? (size_t)d * ld : (size_t)nchains * ld;
+    double *dcols = nullptr, *dx = nullptr, *dlp = nullptr, *dg = nullptr;
+    hipStream_t st = ctx->stream;
     int rc = MCMC_OK;
     do {
-        if ((rc = dmalloc(&dx, (size_t)d * nchains))) break;
+        if ((rc = dmalloc(&dcols, (size_t)d * nchains))) break;
+        if ((rc = dmalloc(&dx, nst))) break;
         if ((rc = dmalloc(&dlp, (size_t)nchains))) break;
-        if (grad && (rc = dmalloc(&dg, (size_t)d * nchains))) break;
-        hipError_t e = hipMemcpy(dx, x, (size_t)d * nchains * 8, hipMemcpyHostToDevice);
-        LpcArgs a = base_args(m, nchains, nchains);
-        if (e == hipSuccess) e = mcmc_launch_lpc_eval(a, dx, nchains, dlp, dg, 0, ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e == hipSuccess) e = hipMemcpy(lp, dlp, (size_t)nchains * 8, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && grad) e = hipMemcpy(grad, dg, (size_t)d * nchains * 8, hipMemcpyDeviceToHost);
+        if (grad && (rc = dmalloc(&dg, nst))) break;
+        hipError_t e = hipMemcpyAsync(dcols, x, (size_t)d * nchains * 8, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = cols_to_state(L, dx, ld, dcols, nchains, d, nchains, st);
+        KernelArgs a = base_args(m, nchains, ld);
+        if (e == hipSuccess) e = launch_eval(L, a, dx, dlp, dg, 0, st);
+        if (e == hipSuccess && grad) e = state_to_cols(L, dcols, nchains, dg, ld, d, nchains, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(lp, dlp, (size_t)nchains * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && grad)
+            e = hipMemcpyAsync(grad, dcols, (size_t)d * nchains * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("model eval: ") + hipGetErrorString(e));
     } while (0);
+    (void)hipStreamSynchronize(st);
+    dfree(dcols);
     dfree(dx);
     dfree(dlp);
     dfree(dg);
@@ -379,10 +419,15 @@ static int init_state(mcmc_chains* c) {
     const SamplerArgs& sa = c->sa;
     hipStream_t st = ctx->stream;
     HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int32_t), st));
-    if (c->d_init_x) HIP_TRY(mcmc_copy_cols(c->st.x, c->ld, c->d_init_x, c->ld, d, c->C, st));
-    else HIP_TRY(mcmc_broadcast_cols(c->st.x, c->ld, m->d_init, d, c->C, st));
-    LpcArgs a = base_args(m, c->C, c->ld);
-    HIP_TRY(mcmc_launch_lpc_eval(a, c->st.x, c->ld, c->st.lp, nullptr, 1, st));
+    if (c->d_init_x) {
+        HIP_TRY(cols_to_state(c->layout, c->st.x, c->ld, c->d_init_x, c->C, d, c->C, st));
+    } else if (c->layout == LAYOUT_LPC) {
+        HIP_TRY(mcmc_broadcast_cols(c->st.x, c->ld, m->d_init, d, c->C, st));
+    } else {
+        HIP_TRY(mcmc_broadcast_rows(c->st.x, c->ld, m->d_init, d, c->C, st));
+    }
+    KernelArgs a = base_args(m, c->C, c->ld);
+    HIP_TRY(launch_eval(c->layout, a, c->st.x, c->st.lp, nullptr, 1, st));
     if (sa.kind == SK_MALA && sa.tuner) HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, sa.drift_step, st));
     if (sa.kind == SK_HMC && sa.tuner) {
         HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, sa.leap_step, st));
@@ -422,15 +467,15 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     mcmc_ctx* ctx = m->ctx;
     if (int r = set_device(ctx)) return r;
     const int d = m->args.d;
-    if (!model_is_separable(m) || d > mcmc_lpc_max_d())
+    if (!model_is_separable(m) || d > mcmc_wpc_max_d())
         return fail(MCMC_E_UNSUPPORTED, "this model x size combination is not built yet");
     auto* c = new mcmc_chains();
     c->model = m;
     c->C = nchains;
-    c->ld = round_up(nchains, 64);
+    c->layout = layout_for(m);
+    c->ld = ld_for(c->layout, nchains, d);
     c->offset = chain_offset;
     c->seed = seed;
-    c->layout = LAYOUT_LPC;
     SamplerArgs& sa = c->sa;
     sa.kind = s->kind;
     sa.tuner = s->tuner;
@@ -452,33 +497,34 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
         mcmc_chains_destroy(c);
         return code;
     };
-    const size_t ld = (size_t)c->ld;
-    if (int r = dmalloc(&c->st.x, (size_t)d * ld)) return bail(r);
-    if (int r = dmalloc(&c->st.lp, ld)) return bail(r);
+    const size_t nst = c->layout == LAYOUT_LPC ? (size_t)d * c->ld : (size_t)nchains * c->ld;
+    const size_t nc = (size_t)round_up(nchains, 64);
+    if (int r = dmalloc(&c->st.x, nst)) return bail(r);
+    if (int r = dmalloc(&c->st.lp, nc)) return bail(r);
     const bool tuned = sa.tuner && (sa.kind == SK_MALA || sa.kind == SK_HMC);
     if (tuned || sa.kind == SK_HMCDA)
-        if (int r = dmalloc(&c->st.t_step, ld)) return bail(r);
+        if (int r = dmalloc(&c->st.t_step, nc)) return bail(r);
     if (sa.kind == SK_HMCDA) {
-        if (int r = dmalloc(&c->st.t_bar, ld)) return bail(r);
-        if (int r = dmalloc(&c->st.t_h, ld)) return bail(r);
+        if (int r = dmalloc(&c->st.t_bar, nc)) return bail(r);
+        if (int r = dmalloc(&c->st.t_h, nc)) return bail(r);
     }
     if (tuned) {
         if (sa.kind == SK_HMC)
-            if (int r = dmalloc(&c->st.t_leaps, ld)) return bail(r);
-        if (int r = dmalloc(&c->st.t_acc, ld)) return bail(r);
-        if (int r = dmalloc(&c->st.t_prop, ld)) return bail(r);
+            if (int r = dmalloc(&c->st.t_leaps, nc)) return bail(r);
+        if (int r = dmalloc(&c->st.t_acc, nc)) return bail(r);
+        if (int r = dmalloc(&c->st.t_prop, nc)) return bail(r);
     }
     // scale = model.scale .* sampler.scale (RWM.jl:52); other samplers do not use it.
     std::vector<double> se(m->scale);
     if (sa.kind == SK_RWM)
         for (auto& v : se) v = v * sa.scale;
-    if (int r = dmalloc(&c->d_scale_eff, (size_t)d)) return bail(r);
-    if (hipMemcpy(c->d_scale_eff, se.data(), (size_t)d * 8, hipMemcpyHostToDevice) != hipSuccess)
+    if (int r = dmalloc(&c->d_scale_eff, (size_t)round_up(d, 256))) return bail(r);
+    if (hipMemset(c->d_scale_eff, 0, (size_t)round_up(d, 256) * 8) != hipSuccess ||
+        hipMemcpy(c->d_scale_eff, se.data(), (size_t)d * 8, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(MCMC_E_HIP, "scale upload failed"));
     if (init_x) {
-        if (int r = dmalloc(&c->d_init_x, (size_t)d * ld)) return bail(r);
-        if (hipMemcpy2D(c->d_init_x, ld * 8, init_x, (size_t)nchains * 8, (size_t)nchains * 8, (size_t)d,
-                        hipMemcpyHostToDevice) != hipSuccess)
+        if (int r = dmalloc(&c->d_init_x, (size_t)d * nchains)) return bail(r);
+        if (hipMemcpy(c->d_init_x, init_x, (size_t)d * nchains * 8, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(MCMC_E_HIP, "init_x upload failed"));
     }
     if (int r = init_state(c)) return bail(r);
@@ -497,6 +543,8 @@ extern "C" int mcmc_chains_destroy(mcmc_chains* c) {
     dfree(c->out_grads.p);
     dfree(c->out_bits.p);
     dfree(c->out_tmp.p);
+    dfree(c->stage_samples.p);
+    dfree(c->stage_grads.p);
     delete c;
     return MCMC_OK;
 }
@@ -535,6 +583,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     hipStream_t st = ctx->stream;
     const int d = m->args.d;
     const int64_t C = c->C;
+    const Layout L = c->layout;
     const int64_t nkept = nkept_of(*r);
     const int64_t nw = (C + 63) / 64;
     if (c->steps_done + r->len > 0xffffffffLL) return fail(MCMC_E_INVALID_ARG, "step counter exceeds 2^32");
@@ -544,6 +593,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     const bool want_grads = out && out->gradients && grad_sampler && c->store_grads;
     const bool want_bits = out && out->accept_bits;
 
+    // output buffers in the C ABI layout ([nkept][d][C]) on the device
     double* d_samples = nullptr;
     double* d_grads = nullptr;
     uint64_t* d_bits = nullptr;
@@ -569,8 +619,22 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
             d_bits = (uint64_t*)c->out_bits.p;
         }
     }
+    // wave-per-chain kernels write kept rows chain-major ([nkept][C][ld]); transposed after the loop
+    double* k_samples = d_samples;
+    double* k_grads = d_grads;
+    if (L == LAYOUT_WPC) {
+        const size_t nstage = (size_t)nkept * (size_t)C * (size_t)c->ld;
+        if (want_samples) {
+            if (int rc = ensure(c->stage_samples, nstage * 8)) return rc;
+            k_samples = (double*)c->stage_samples.p;
+        }
+        if (want_grads) {
+            if (int rc = ensure(c->stage_grads, nstage * 8)) return rc;
+            k_grads = (double*)c->stage_grads.p;
+        }
+    }
 
-    LpcArgs a = base_args(m, C, c->ld);
+    KernelArgs a = base_args(m, C, c->ld);
     a.sa = c->sa;
     a.st = c->st;
     StepArgs& s = a.s;
@@ -583,8 +647,8 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     s.len = r->len;
     s.tuner_burnin = r->burnin;
     s.scale = c->d_scale_eff;
-    s.samples = d_samples;
-    s.grads = d_grads;
+    s.samples = k_samples;
+    s.grads = k_grads;
     s.acc_bits = d_bits;
     s.nw = nw;
 
@@ -592,14 +656,19 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     HIP_TRY(hipStreamSynchronize(st));
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventRecord(ctx->ev0, st));
+    if (want_bits && L == LAYOUT_WPC) HIP_TRY(hipMemsetAsync(d_bits, 0, (size_t)nkept * nw * 8, st));
     for (int64_t done = 0; done < r->len; done += spl) {
         const int64_t n = std::min(spl, r->len - done);
         s.step_begin = c->steps_done + done + 1;
         s.nsteps = (int32_t)n;
-        HIP_TRY(mcmc_launch_lpc_step(a, st));
+        HIP_TRY(launch_step(L, a, st));
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
-    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    if (L == LAYOUT_WPC) {
+        if (want_samples) HIP_TRY(mcmc_transpose(d_samples, C, k_samples, c->ld, nkept, C, d, st));
+        if (want_grads) HIP_TRY(mcmc_transpose(d_grads, C, k_grads, c->ld, nkept, C, d, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
     auto t1 = std::chrono::steady_clock::now();
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -615,13 +684,17 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
             if (want_bits) HIP_TRY(hipMemcpy(out->accept_bits, d_bits, (size_t)nkept * nw * 8, hipMemcpyDeviceToHost));
         }
         if (out->final_x) {
-            if (on_dev) HIP_TRY(mcmc_copy_cols(out->final_x, C, c->st.x, c->ld, d, C, st));
-            else HIP_TRY(hipMemcpy2D(out->final_x, (size_t)C * 8, c->st.x, (size_t)c->ld * 8, (size_t)C * 8, (size_t)d,
-                                     hipMemcpyDeviceToHost));
+            if (on_dev) {
+                HIP_TRY(state_to_cols(L, out->final_x, C, c->st.x, c->ld, d, C, st));
+            } else {
+                if (int rc = ensure(c->out_tmp, (size_t)d * C * 8)) return rc;
+                HIP_TRY(state_to_cols(L, (double*)c->out_tmp.p, C, c->st.x, c->ld, d, C, st));
+                HIP_TRY(hipMemcpyAsync(out->final_x, c->out_tmp.p, (size_t)d * C * 8, hipMemcpyDeviceToHost, st));
+            }
         }
         if (out->final_lp)
-            HIP_TRY(hipMemcpy(out->final_lp, c->st.lp, (size_t)C * 8,
-                              on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpyAsync(out->final_lp, c->st.lp, (size_t)C * 8,
+                                   on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
     return MCMC_OK;

@@ -19,27 +19,34 @@ __global__ void k_broadcast_cols(double* dst, int64_t ldd, const double* v, int 
     if (c >= C) return;
     for (int j = 0; j < d; ++j) dst[(size_t)j * ldd + c] = v[j];
 }
+// dst[c][j] (row stride ldr) <- v[j]  (chain-major layout of the wave-per-chain kernels)
+__global__ void k_broadcast_rows(double* dst, int64_t ldr, const double* v, int d, int64_t C) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C * (int64_t)ldr) return;
+    const int64_t j = i % ldr;
+    dst[i] = j < d ? v[j] : 0.0;
+}
 // dst[j][c] (stride ldd) <- src[j][c] (stride lds)
 __global__ void k_copy_cols(double* dst, int64_t ldd, const double* src, int64_t lds, int d, int64_t C) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     for (int j = 0; j < d; ++j) dst[(size_t)j * ldd + c] = src[(size_t)j * lds + c];
 }
-// Tiled transpose of R x S row-major matrices, batched: dst[b][s][r] <- src[b][r][s].
-__global__ void k_transpose(double* dst, const double* src, int64_t R, int64_t S) {
+// Tiled transpose, batched: dst[b][s][r] (row stride ldd) <- src[b][r][s] (row stride lds).
+__global__ void k_transpose(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t R, int64_t S) {
     __shared__ double tile[32][33];
     const int64_t b = blockIdx.z;
-    const int64_t r0 = (int64_t)blockIdx.y * 32, s0 = (int64_t)blockIdx.x * 32;
-    const double* sb = src + (size_t)b * R * S;
-    double* db = dst + (size_t)b * R * S;
+    const int64_t r0 = (int64_t)blockIdx.x * 32, s0 = (int64_t)blockIdx.y * 32;
+    const double* sb = src + (size_t)b * (size_t)R * (size_t)lds;
+    double* db = dst + (size_t)b * (size_t)S * (size_t)ldd;
     for (int k = threadIdx.y; k < 32; k += blockDim.y) {
         const int64_t r = r0 + k, s = s0 + threadIdx.x;
-        if (r < R && s < S) tile[k][threadIdx.x] = sb[(size_t)r * S + s];
+        if (r < R && s < S) tile[k][threadIdx.x] = sb[(size_t)r * lds + s];
     }
     __syncthreads();
     for (int k = threadIdx.y; k < 32; k += blockDim.y) {
         const int64_t s = s0 + k, r = r0 + threadIdx.x;
-        if (r < R && s < S) db[(size_t)s * R + r] = tile[threadIdx.x][k];
+        if (r < R && s < S) db[(size_t)s * ldd + r] = tile[threadIdx.x][k];
     }
 }
 
@@ -98,15 +105,26 @@ hipError_t mcmc_broadcast_cols(double* dst, int64_t ldd, const double* v, int d,
     mcmc::k_broadcast_cols<<<nblk(C, 256), 256, 0, st>>>(dst, ldd, v, d, C);
     return hipGetLastError();
 }
+hipError_t mcmc_broadcast_rows(double* dst, int64_t ldr, const double* v, int d, int64_t C, hipStream_t st) {
+    mcmc::k_broadcast_rows<<<nblk(C * ldr, 256), 256, 0, st>>>(dst, ldr, v, d, C);
+    return hipGetLastError();
+}
 hipError_t mcmc_copy_cols(double* dst, int64_t ldd, const double* src, int64_t lds, int d, int64_t C, hipStream_t st) {
     mcmc::k_copy_cols<<<nblk(C, 256), 256, 0, st>>>(dst, ldd, src, lds, d, C);
     return hipGetLastError();
 }
-hipError_t mcmc_transpose(double* dst, const double* src, int64_t batch, int64_t R, int64_t S, hipStream_t st) {
+hipError_t mcmc_transpose(double* dst, int64_t ldd, const double* src, int64_t lds, int64_t batch, int64_t R,
+                          int64_t S, hipStream_t st) {
     if (batch <= 0 || R <= 0 || S <= 0) return hipSuccess;
-    const dim3 grid(nblk(S, 32), nblk(R, 32), (unsigned)batch);
-    mcmc::k_transpose<<<grid, dim3(32, 8), 0, st>>>(dst, src, R, S);
-    return hipGetLastError();
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+        const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+        const dim3 grid(nblk(R, 32), nblk(S, 32), (unsigned)nb);
+        mcmc::k_transpose<<<grid, dim3(32, 8), 0, st>>>(dst + (size_t)b0 * S * ldd, ldd,
+                                                        src + (size_t)b0 * R * lds, lds, R, S);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 hipError_t mcmc_detmath(int op, int64_t n, const double* x, const double* y, double* out, hipStream_t st) {
     mcmc::k_detmath<<<nblk(n, 256), 256, 0, st>>>(op, n, x, y, out);

@@ -1,0 +1,475 @@
+// samplers.hpp -- fused multi-step sampler kernels, generic over the chain->lane mapping.
+//
+// A kernel launch advances every chain by `nsteps` steps of the SerialMC loop
+// (SerialMC.jl:47-67) with the chain state held in VGPRs; HBM sees the state
+// once per launch plus the kept samples/gradients and the accept bits.
+//
+// Two mappings (policies) share the step code:
+//   LaneChain<NB>  one thread = one chain, coordinates j = 0..4NB-1 in registers,
+//                  state SoA x[j][c] (coalesced across the wave), sums in order
+//                  j = 0,1,... (oracle order 0).  d <= 32.
+//   WaveChain<G>   one wave = one chain, lane l owns coordinates 4(l+64k)+e
+//                  (k < G, e < 4), state chain-major x[c][j] read as 2 x 16 B per
+//                  lane, sums = per-lane partial then xor butterfly over the wave
+//                  (oracle order 1).  32 < d <= 2048.
+// Both draw coordinate j's normal from Philox block j/4, slot j%4 of
+// (chain, step, block, TAG_NORMAL), so the chain's random stream does not
+// depend on the mapping.
+//
+// Per step (reference file:line for each sampler):
+//   RWM    RWM.jl:58-71      x' = x + randn .* scale; accept iff r > 0 || r > log(rand())
+//   MALA   MALA.jl:89-125    Langevin proposal, forward/backward densities, EmpMCTuner
+//   HMC    HMC.jl:252-299    L leapfrogs (HMC.jl:219-228), accept iff rand() < exp(H0 - H)
+//   HMCDA  HMCDA.jl:97-142   nLeaps = max(1, round(len/eps)), p = min(1, exp(H0-H)),
+//                            dual averaging while i < burnin
+#pragma once
+#include "common.hpp"
+#include "detmath.hpp"
+#include "models.hpp"
+#include "host/kernels_api.hpp"
+
+namespace mcmc {
+
+constexpr int kBlock = 256;
+
+// ------------------------------------------------------------------ mappings
+template <int NB_>
+struct LaneChain {
+    static constexpr int NB = NB_;
+    static constexpr int NC = 4 * NB_;
+    int64_t c;        // local chain index
+    bool live;        // c < C
+    int d;
+    __device__ LaneChain(const StepArgs& s) {
+        c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        live = c < s.C;
+        d = s.d;
+    }
+    __device__ __forceinline__ int coord(int k) const { return k; }
+    __device__ __forceinline__ bool valid(int k) const { return k < d; }
+    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)b; }
+    __device__ __forceinline__ double reduce(double v) const { return v; }
+    __device__ __forceinline__ void load(const double* x, int64_t ld, double (&v)[NC]) const {
+        const int64_t cc = live ? c : 0;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) v[k] = valid(k) ? x[(size_t)k * ld + cc] : 0.0;
+    }
+    __device__ __forceinline__ void store(double* x, int64_t ld, const double (&v)[NC]) const {
+        if (!live) return;
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (valid(k)) x[(size_t)k * ld + c] = v[k];
+    }
+    __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ T load_t(const T* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ void store_t(T* p, T v) const {
+        if (live) p[c] = v;
+    }
+    // kept sample in the C ABI layout [nkept][d][C]
+    __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
+                                               double* base) const {
+        if (base == nullptr || !live) return;
+        double* p = base + (size_t)kk * (size_t)d * (size_t)s.C + (size_t)c;
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (valid(k)) p[(size_t)k * (size_t)s.C] = v[k];
+    }
+    __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
+        const uint64_t mask = __ballot(acc && live);
+        if ((threadIdx.x & 63) == 0 && s.acc_bits != nullptr) {
+            const int64_t w = c >> 6;
+            if (w < s.nw) s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)w] = mask;
+        }
+    }
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int G>
+struct WaveChain {
+    static constexpr int NB = G;
+    static constexpr int NC = 4 * G;
+    int64_t c;
+    bool live;
+    int d;
+    int lane;
+    int64_t ldr;      // row stride of chain-major state (multiple of 4)
+    __device__ WaveChain(const StepArgs& s) {
+        c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        live = c < s.C;
+        d = s.d;
+        lane = threadIdx.x & 63;
+        ldr = s.ld;
+    }
+    __device__ __forceinline__ int coord(int k) const { return 4 * (lane + 64 * (k >> 2)) + (k & 3); }
+    __device__ __forceinline__ bool valid(int k) const { return coord(k) < d; }
+    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + 64 * b); }
+    __device__ __forceinline__ double reduce(double v) const { return wave_sum(v); }
+    __device__ __forceinline__ void load(const double* x, int64_t /*ld*/, double (&v)[NC]) const {
+        const double* row = x + (size_t)(live ? c : 0) * (size_t)ldr;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = 4 * (lane + 64 * g);
+            if (j0 < d) {
+                const double4 q = *reinterpret_cast<const double4*>(row + j0);
+                v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+            } else {
+                v[4 * g] = v[4 * g + 1] = v[4 * g + 2] = v[4 * g + 3] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (!valid(k)) v[k] = 0.0;
+    }
+    __device__ __forceinline__ void store(double* x, int64_t /*ld*/, const double (&v)[NC]) const {
+        if (!live) return;
+        double* row = x + (size_t)c * (size_t)ldr;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = 4 * (lane + 64 * g);
+            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
+                                                                               v[4 * g + 3]);
+        }
+    }
+    __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ T load_t(const T* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ void store_t(T* p, T v) const {
+        if (live && lane == 0) p[c] = v;
+    }
+    // kept sample into the chain-major staging layout [nkept][C][ldr] (transposed to the C ABI
+    // layout after the step loop)
+    __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
+                                               double* base) const {
+        if (base == nullptr || !live) return;
+        double* row = base + ((size_t)kk * (size_t)s.C + (size_t)c) * (size_t)ldr;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = 4 * (lane + 64 * g);
+            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
+                                                                               v[4 * g + 3]);
+        }
+    }
+    __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
+        if (live && lane == 0 && acc && s.acc_bits != nullptr)
+            atomicOr((unsigned long long*)&s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)(c >> 6)],
+                     1ull << (c & 63));
+    }
+};
+
+// ------------------------------------------------------------------ shared pieces
+template <class P>
+__device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32_t chain, uint32_t step,
+                                            double (&z)[P::NC]) {
+#pragma unroll
+    for (int b = 0; b < P::NB; ++b) {
+        const u32x4 w = rs.block(chain, step, p.block(b), TAG_NORMAL);
+        normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3]);
+    }
+}
+
+template <class P, class M>
+__device__ __forceinline__ double eval_lp(const P& p, const M& model, const double (&v)[P::NC], bool& oos) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < P::NC; ++k)
+        if (p.valid(k)) model.acc(a, v[k]);
+    return llacc_finish(model, p.reduce(a), oos);
+}
+
+template <class P>
+__device__ __forceinline__ double half_dot(const P& p, const double (&m)[P::NC]) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < P::NC; ++k)
+        if (p.valid(k)) a = __builtin_fma(m[k], m[k], a);
+    return 0.5 * p.reduce(a);
+}
+
+__device__ __forceinline__ bool mh_accept_short_circuit(const Stream& rs, uint32_t chain, uint32_t step, double ratio) {
+    // RWM.jl:63 / MALA.jl:108: ratio > 0 || ratio > log(rand()); the uniform is drawn only if needed.
+    bool acc = ratio > 0.0;
+    if (!acc) {
+        const u32x4 w = rs.block(chain, step, 0u, TAG_ACCEPT);
+        acc = ratio > det_log(uniform53(w.x, w.y));
+    }
+    return acc;
+}
+
+// tuner adaptation factor (MALA.jl:36-39, HMC.jl:165-169)
+__device__ __forceinline__ double tune_factor(int32_t acc, int32_t prop, double target) {
+    const double rate = (double)acc / (double)prop;
+    return 1.0 / (1.0 + det_exp(-11.0 * (rate - target))) + 0.5;
+}
+
+// ------------------------------------------------------------------ RWM
+template <class P, class M>
+__device__ __forceinline__ void rwm_body(const KernelArgs& a) {
+    const StepArgs& s = a.s;
+    const P p(s);
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    double x[P::NC], sc[P::NC];
+    p.load(a.st.x, s.ld, x);
+#pragma unroll
+    for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? s.scale[p.coord(k)] : 0.0;
+    double lp = p.load_scalar(a.st.lp);
+
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        double xp[P::NC];
+        gen_normals(p, rs, chain, (uint32_t)i, xp);             // xp <- z
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) xp[k] = x[k] + xp[k] * sc[k];   // pars + randn(d) .* scale
+        bool oos;
+        const double lpp = eval_lp(p, model, xp, oos);
+        const double ratio = lpp - lp;
+        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        if (acc) {
+#pragma unroll
+            for (int k = 0; k < P::NC; ++k) x[k] = xp[k];
+            lp = lpp;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            p.store_kept(s, kk, x, s.samples);
+            p.store_bit(s, kk, acc);
+        }
+    }
+    p.store(a.st.x, s.ld, x);
+    p.store_t(a.st.lp, lp);
+}
+
+// ------------------------------------------------------------------ MALA
+template <class P, class M>
+__device__ __forceinline__ void mala_body(const KernelArgs& a) {
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const P p(s);
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    double x[P::NC];
+    p.load(a.st.x, s.ld, x);
+    double lp = p.load_scalar(a.st.lp);
+    double h = sa.tuner ? p.load_scalar(a.st.t_step) : sa.drift_step;
+    int32_t n_acc = sa.tuner ? p.load_t(a.st.t_acc) : 0;
+    int32_t n_prop = sa.tuner ? p.load_t(a.st.t_prop) : 0;
+
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        if (sa.tuner) n_prop += 1;
+        const double half = h / 2.0;
+        const double sq = __builtin_sqrt(h);
+        const double twoh = 2.0 * h;
+        const double L = det_log(kTwoPi * h) / 2.0;             // log(2*pi*driftStep)/2
+        double xp[P::NC];
+        gen_normals(p, rs, chain, (uint32_t)i, xp);
+        double qf = 0.0;
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            const double pm = x[k] + half * model.grad(x[k]);   // parsMean (MALA.jl:98)
+            xp[k] = pm + sq * xp[k];                            // MALA.jl:100
+            const double e = pm - xp[k];
+            if (p.valid(k)) qf = qf + ((-(e * e)) / twoh - L);  // MALA.jl:103
+        }
+        qf = p.reduce(qf);
+        bool oos;
+        const double lpp = eval_lp(p, model, xp, oos);
+        double qb = 0.0;
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            const double gp = oos ? 0.0 : model.grad(xp[k]);
+            const double e = (xp[k] + half * gp) - x[k];       // MALA.jl:104-105
+            if (p.valid(k)) qb = qb + ((-(e * e)) / twoh - L);
+        }
+        qb = p.reduce(qb);
+        const double ratio = ((lpp + qb) - lp) - qf;            // MALA.jl:107
+        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        if (acc) {
+#pragma unroll
+            for (int k = 0; k < P::NC; ++k) x[k] = xp[k];
+            lp = lpp;
+            if (sa.tuner) n_acc += 1;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            p.store_kept(s, kk, x, s.samples);
+            if (s.grads != nullptr) {
+                double g[P::NC];
+#pragma unroll
+                for (int k = 0; k < P::NC; ++k) g[k] = model.grad(x[k]);
+                p.store_kept(s, kk, g, s.grads);
+            }
+            p.store_bit(s, kk, acc);
+        }
+        if (sa.tuner && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // MALA.jl:116-118
+            h = h * tune_factor(n_acc, n_prop, sa.target_rate);
+            n_acc = 0;
+            n_prop = 0;
+        }
+    }
+    p.store(a.st.x, s.ld, x);
+    p.store_t(a.st.lp, lp);
+    if (sa.tuner) {
+        p.store_t(a.st.t_step, h);
+        p.store_t(a.st.t_acc, n_acc);
+        p.store_t(a.st.t_prop, n_prop);
+    }
+}
+
+// ------------------------------------------------------------------ HMC / HMCDA
+// nl leapfrogs from (x, m) (HMC.jl:219-228); the start point is in support.
+template <class P, class M>
+__device__ __forceinline__ double trajectory(const P& p, const M& model, double eps, int64_t nl, double (&x)[P::NC],
+                                             double (&m)[P::NC]) {
+    bool oos = false;
+    double lpl = 0.0;
+    for (int64_t l = 0; l < nl; ++l) {
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            const double g = oos ? 0.0 : model.grad(x[k]);
+            m[k] = m[k] + (0.5 * g) * eps;                      // n.m += 0.5*n.grad*ve
+            x[k] = x[k] + eps * m[k];                           // n.pars += ve * n.m
+        }
+        lpl = eval_lp(p, model, x, oos);                        // calc!(n, ll)
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            const double g = oos ? 0.0 : model.grad(x[k]);
+            m[k] = m[k] + (0.5 * g) * eps;
+        }
+    }
+    return lpl;
+}
+
+template <class P, class M, bool DA>
+__device__ __forceinline__ void hmc_body(const KernelArgs& a) {
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const P p(s);
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int64_t max_leaps = sa.max_leaps;
+    const bool tuned = !DA && sa.tuner;
+
+    double x0[P::NC];
+    p.load(a.st.x, s.ld, x0);
+    double lp = p.load_scalar(a.st.lp);
+    double eps = (DA || tuned) ? p.load_scalar(a.st.t_step) : sa.leap_step;
+    int64_t nl_fixed = tuned ? (int64_t)p.load_t(a.st.t_leaps) : sa.n_leaps;
+    double eps_bar = DA ? p.load_scalar(a.st.t_bar) : 0.0;
+    double h_bar = DA ? p.load_scalar(a.st.t_h) : 0.0;
+    int32_t n_acc = tuned ? p.load_t(a.st.t_acc) : 0;
+    int32_t n_prop = tuned ? p.load_t(a.st.t_prop) : 0;
+    const double mu = DA ? det_log(10.0) : 0.0;                 // log(10*leapStep0), leapStep0 = 1
+
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        if (tuned) n_prop += 1;
+        double m[P::NC], x[P::NC];
+        gen_normals(p, rs, chain, (uint32_t)i, m);              // state0.m = randn(model.size)
+        const double H0 = -lp + half_dot(p, m);                 // update!(state0)
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) x[k] = x0[k];
+        int64_t nl;
+        if (DA) {
+            const double r = round_away(sa.len / eps);          // HMCDA.jl:104
+            nl = r < 1.0 ? 1 : (r > (double)max_leaps ? max_leaps : (int64_t)r);
+        } else {
+            nl = nl_fixed;
+        }
+        const double lpl = trajectory(p, model, eps, nl, x, m);
+        const double H = -lpl + half_dot(p, m);
+        const u32x4 w = rs.block(chain, (uint32_t)i, 0u, TAG_ACCEPT);
+        const double u = uniform53(w.x, w.y);
+        bool acc;
+        double pa = 0.0;
+        if (DA) {
+            pa = __builtin_fmin(1.0, det_exp(H0 - H));          // HMCDA.jl:120 (Julia 0.2 min: NaN-ignoring)
+            acc = u < pa;
+        } else {
+            acc = u < det_exp(H0 - H);                          // HMC.jl:280
+        }
+        if (acc) {
+#pragma unroll
+            for (int k = 0; k < P::NC; ++k) x0[k] = x[k];
+            lp = lpl;
+            if (tuned) n_acc += 1;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            p.store_kept(s, kk, x0, s.samples);
+            if (s.grads != nullptr) {
+                double g[P::NC];
+#pragma unroll
+                for (int k = 0; k < P::NC; ++k) g[k] = model.grad(x0[k]);
+                p.store_kept(s, kk, g, s.grads);
+            }
+            p.store_bit(s, kk, acc);
+        }
+        if (DA) {
+            const double di = (double)i;
+            if (di < (double)s.tuner_burnin) {                  // HMCDA.jl:133-138
+                double eta = 1.0 / (di + sa.t0);
+                h_bar = (1.0 - eta) * h_bar + eta * (sa.rate - pa);
+                eps = det_exp(mu - (__builtin_sqrt(di) * h_bar) / sa.shrinkage);
+                eta = det_exp(det_log(di) * (-sa.step));        // i^(-step)
+                eps_bar = det_exp((1.0 - eta) * det_log(eps_bar) + eta * det_log(eps));
+            } else {
+                eps = eps_bar;                                  // HMCDA.jl:140
+            }
+        } else if (tuned && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // HMC.jl:293-295
+            eps = eps * tune_factor(n_acc, n_prop, sa.target_rate);
+            double nlf = __builtin_ceil(sa.target_path / eps);
+            if (nlf > (double)sa.max_step) nlf = (double)sa.max_step;
+            if (nlf > (double)max_leaps) nlf = (double)max_leaps;
+            nl_fixed = (int64_t)nlf;
+            n_acc = 0;
+            n_prop = 0;
+        }
+    }
+    p.store(a.st.x, s.ld, x0);
+    p.store_t(a.st.lp, lp);
+    if (DA || tuned) p.store_t(a.st.t_step, eps);
+    if (DA) {
+        p.store_t(a.st.t_bar, eps_bar);
+        p.store_t(a.st.t_h, h_bar);
+    } else if (tuned) {
+        p.store_t(a.st.t_leaps, (int32_t)nl_fixed);
+        p.store_t(a.st.t_acc, n_acc);
+        p.store_t(a.st.t_prop, n_prop);
+    }
+}
+
+// ------------------------------------------------------------------ eval
+// lp (and gradient) of x; flags out-of-support starts (RWM.jl:54-55).
+template <class P, class M>
+__device__ __forceinline__ void eval_body(const KernelArgs& a, const double* xin, double* lp_out, double* g_out,
+                                          int32_t check) {
+    const StepArgs& s = a.s;
+    const P p(s);
+    const M model(a.m);
+    double x[P::NC];
+    p.load(xin, s.ld, x);
+    bool oos;
+    const double lp = eval_lp(p, model, x, oos);
+    p.store_t(lp_out, lp);
+    if (g_out != nullptr) {
+        double g[P::NC];
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) g[k] = oos ? 0.0 : model.grad(x[k]);
+        p.store(g_out, s.ld, g);
+    }
+    if (check && p.live && !(lp - lp == 0.0)) atomicOr(s.err, 1);
+}
+
+}  // namespace mcmc

@@ -110,30 +110,36 @@ def assert_parity(chain, s_ref, g_ref, acc_ref, kind):
         np.testing.assert_allclose(chain._gradients, g_ref, rtol=RTOL, atol=0)
 
 
+def order_for(d):
+    """lane-per-chain kernels (d <= 32) sum left to right; wave-per-chain kernels per lane + butterfly."""
+    return 0 if d <= 32 else 1
+
+
 @pytest.mark.parametrize("sname", list(SAMPLERS))
 @pytest.mark.parametrize("mkind", ["iso", "normal"])
-@pytest.mark.parametrize("d", [1, 3, 7, 16, 32])
+@pytest.mark.parametrize("d", [1, 3, 7, 16, 32, 33, 100, 256, 257, 1024])
 def test_sampler_parity(gpu, sname, mkind, d):
     m = _model(mkind, d)
-    C = 200                                              # not a multiple of 64: tail wave
-    r = mc.SerialMC(steps=45, burnin=6, thinning=3)
+    C = 200 if d <= 256 else 67                          # not a multiple of 64 / of 4: tail wave, tail block
+    r = mc.SerialMC(steps=45 if d <= 256 else 20, burnin=6, thinning=3)
     task = m * SAMPLERS[sname]() * r
     chain = mc.run(task, nchains=C, seed=12345 + d)
-    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=C, seed=12345 + d)
+    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=C, seed=12345 + d, order=order_for(d))
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
     assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
 
 
+@pytest.mark.parametrize("d", [5, 70])
 @pytest.mark.parametrize("sname", ["rwm", "mala_tuned", "hmc_tuned", "hmcda"])
-def test_continue_run_matches_oracle(gpu, sname):
+def test_continue_run_matches_oracle(gpu, sname, d):
     """run(chain) continues the same chains (runners.jl:14); tuners keep adapting only while i <= burnin."""
-    m = _model("normal", 5)
+    m = _model("normal", d)
     r = mc.SerialMC(steps=30, burnin=12, thinning=2)
     task = (m * SAMPLERS[sname]() * r).batch(130, seed=77)
     c1 = mc.run(task)
     c2 = mc.run(c1)
-    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=130, seed=77)
+    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=130, seed=77, order=order_for(d))
     s1, g1, a1 = oc.run(r)
     s2, g2, a2 = oc.run(r)
     assert_parity(c1, s1, g1, a1, sname)
@@ -141,9 +147,10 @@ def test_continue_run_matches_oracle(gpu, sname):
     assert task.steps_done == 60
 
 
+@pytest.mark.parametrize("d", [8, 96])
 @pytest.mark.parametrize("spl", [1, 7])
-def test_steps_per_launch_is_invisible(gpu, spl):
-    m = _model("iso", 8)
+def test_steps_per_launch_is_invisible(gpu, spl, d):
+    m = _model("iso", d)
     r = mc.SerialMC(steps=40, burnin=5, thinning=4)
     a = mc.run((m * mc.MALA(0.3) * r).batch(150, seed=3))
     b = mc.run((m * mc.MALA(0.3) * r).batch(150, seed=3, steps_per_launch=spl))
@@ -151,8 +158,9 @@ def test_steps_per_launch_is_invisible(gpu, spl):
     assert np.array_equal(a.diagnostics["accept"], b.diagnostics["accept"])
 
 
-def test_chain_offset_sharding_is_invisible(gpu):
-    m = _model("iso", 4)
+@pytest.mark.parametrize("d", [4, 130])
+def test_chain_offset_sharding_is_invisible(gpu, d):
+    m = _model("iso", d)
     r = mc.SerialMC(steps=25, burnin=3)
     full = mc.run((m * mc.HMC(3, 0.25) * r).batch(300, seed=5))
     lo = mc.run((m * mc.HMC(3, 0.25) * r).batch(170, seed=5, chain_offset=0))
@@ -182,12 +190,13 @@ def test_resume_restarts_from_init(gpu):
     assert ch2.samples.shape == (64, 15, 3) and ch2.task.steps_done == 30
 
 
-def test_model_eval_matches_oracle(gpu):
+@pytest.mark.parametrize("d", [9, 300])
+def test_model_eval_matches_oracle(gpu, d):
     for kind in ("iso", "normal"):
-        m = _model(kind, 9)
-        x = np.random.default_rng(0).normal(size=(9, 333)) * 3
+        m = _model(kind, d)
+        x = np.random.default_rng(0).normal(size=(d, 333)) * 3
         lp, g = m.evalallg(x)
-        lp_r, g_r = orc.eval_batch(m, x)
+        lp_r, g_r = orc.eval_batch(m, x, order=order_for(d))
         assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
 
 
@@ -200,12 +209,13 @@ def test_init_out_of_support(gpu):
         mc.model(mc.NormalDSL(0, 1), v=np.array([np.inf]), gradient=True)._handle(0)
 
 
-def test_divergent_hmc_rejects(gpu):
+@pytest.mark.parametrize("d", [4, 40])
+def test_divergent_hmc_rejects(gpu, d):
     """Huge leapfrog steps on the DSL target: out-of-support trajectories (-Inf, zero grad) must reject."""
-    m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.ones(4), gradient=True)
+    m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.ones(d), gradient=True)
     r = mc.SerialMC(steps=20)
     ch = mc.run((m * mc.HMC(30, 1e150) * r).batch(70, seed=4))
-    oc = orc.OracleChains(m, mc.HMC(30, 1e150), nchains=70, seed=4)
+    oc = orc.OracleChains(m, mc.HMC(30, 1e150), nchains=70, seed=4, order=order_for(d))
     s, g, acc = oc.run(r)
     assert_parity(ch, s, g, acc, "hmc")
     assert not ch.diagnostics["accept"].any()
