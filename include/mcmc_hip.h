@@ -175,6 +175,9 @@ int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_o
 int mcmc_debug_detmath(mcmc_ctx* ctx, int op, int64_t n, const double* x, const double* y, double* out);
 int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr /*[n][4]*/, const uint32_t* key /*[n][2]*/,
                       uint32_t* out /*[n][4]*/);
+/* nk chained v_mfma_f64_16x16x4_f64: D = A[16][4nk] * B[4nk][16] + C[16][16] (row-major, host pointers);
+   pins the fp64 MFMA accumulation order the regression kernels rely on. */
+int mcmc_debug_mfma_f64(mcmc_ctx* ctx, int nk, const double* A, const double* B, const double* C, double* D);
 
 #ifdef __cplusplus
 }

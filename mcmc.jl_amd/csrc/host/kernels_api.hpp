@@ -24,6 +24,11 @@ hipError_t mcmc_launch_wpc_step(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_wpc_max_d();
+// regression models on fp64 MFMA, state [d][ld] (+ gradient [d][ld])
+hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
+                                hipStream_t st);
+int mcmc_glm_max_d();
 
 hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st);
 hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st);
@@ -35,3 +40,4 @@ hipError_t mcmc_transpose(double* dst, int64_t ldd, const double* src, int64_t l
                           int64_t S, hipStream_t st);
 hipError_t mcmc_detmath(int op, int64_t n, const double* x, const double* y, double* out, hipStream_t st);
 hipError_t mcmc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out, hipStream_t st);
+hipError_t mcmc_mfma_probe(const double* A, const double* B, const double* C, double* D, int nk, hipStream_t st);

@@ -66,7 +66,7 @@ struct mcmc_model {
     double* d_Y = nullptr;
 };
 
-enum Layout { LAYOUT_LPC = 0, LAYOUT_WPC = 1 };
+enum Layout { LAYOUT_LPC = 0, LAYOUT_WPC = 1, LAYOUT_GLM = 2 };
 
 struct DevBuf {
     void* p = nullptr;
@@ -286,8 +286,37 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
             if (!(desc->sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "Normal sigma should be > 0"));
             break;
         case MCMC_MODEL_LOGISTIC:
-        case MCMC_MODEL_LINEAR:
-            return bail(fail(MCMC_E_UNSUPPORTED, "regression models are not built in this library version"));
+        case MCMC_MODEL_LINEAR: {
+            if (d > mcmc_glm_max_d()) return bail(fail(MCMC_E_UNSUPPORTED, "regression models support d <= 512"));
+            if (desc->n <= 0 || !desc->X || !desc->Y) return bail(fail(MCMC_E_INVALID_ARG, "regression needs n > 0, X, Y"));
+            if (!(desc->prior_sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "prior sigma should be > 0"));
+            if (desc->kind == MCMC_MODEL_LINEAR && !(desc->noise_sigma > 0))
+                return bail(fail(MCMC_E_INVALID_ARG, "noise sigma should be > 0"));
+            if (desc->kind == MCMC_MODEL_LOGISTIC && !(desc->link_sign == 1.0 || desc->link_sign == -1.0))
+                return bail(fail(MCMC_E_INVALID_ARG, "link_sign must be +1 or -1"));
+            if (desc->kind == MCMC_MODEL_LOGISTIC)
+                for (int64_t i = 0; i < desc->n; ++i)
+                    if (!(desc->Y[i] == 0.0 || desc->Y[i] == 1.0))
+                        return bail(fail(MCMC_E_INVALID_ARG, "logistic responses must be 0 or 1 (Bernoulli)"));
+            // X_pad [n_pad][d_pad] row-major, zero rows/columns past (n, d) (glm.hip geometry)
+            const int64_t d_pad = d <= 128 ? (d + 15) / 16 * 16 : (d + 127) / 128 * 128;
+            const int64_t n_pad = (desc->n + 15) / 16 * 16;
+            std::vector<double> Xp((size_t)n_pad * d_pad, 0.0), Yp((size_t)n_pad, 0.0);
+            for (int64_t i = 0; i < desc->n; ++i) {
+                for (int64_t k = 0; k < d; ++k) Xp[(size_t)i * d_pad + k] = desc->X[(size_t)i * d + k];
+                Yp[(size_t)i] = desc->Y[i];
+            }
+            if (int r = dmalloc(&m->d_X, Xp.size())) return bail(r);
+            if (int r = dmalloc(&m->d_Y, Yp.size())) return bail(r);
+            if (hipMemcpy(m->d_X, Xp.data(), Xp.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(m->d_Y, Yp.data(), Yp.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(MCMC_E_HIP, "model data upload failed"));
+            a.n = desc->n;
+            a.n_pad = n_pad;
+            a.X = m->d_X;
+            a.Y = m->d_Y;
+            break;
+        }
         default:
             return bail(fail(MCMC_E_UNSUPPORTED, "unknown model kind"));
     }
@@ -321,14 +350,16 @@ extern "C" int mcmc_model_destroy(mcmc_model* m) {
 static bool model_is_separable(const mcmc_model* m) {
     return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL;
 }
+static bool model_is_glm(const mcmc_model* m) { return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR; }
 
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
 // State layout of a chain batch: lane-per-chain [d][ld] for d <= 32, wave-per-chain [C][ld] above.
 static Layout layout_for(const mcmc_model* m) {
+    if (model_is_glm(m)) return LAYOUT_GLM;
     return m->args.d <= mcmc_lpc_max_d() ? LAYOUT_LPC : LAYOUT_WPC;
 }
-static int64_t ld_for(Layout L, int64_t C, int d) { return L == LAYOUT_LPC ? round_up(C, 64) : round_up(d, 4); }
+static int64_t ld_for(Layout L, int64_t C, int d) { return L == LAYOUT_WPC ? round_up(d, 4) : round_up(C, 64); }
 
 static KernelArgs base_args(const mcmc_model* m, int64_t C, int64_t ld) {
     KernelArgs a{};
@@ -343,17 +374,19 @@ static KernelArgs base_args(const mcmc_model* m, int64_t C, int64_t ld) {
 
 static hipError_t launch_eval(Layout L, const KernelArgs& a, const double* xin, double* lp, double* g, int check,
                               hipStream_t st) {
+    if (L == LAYOUT_GLM) return mcmc_launch_glm_eval(a, xin, lp, g, check, st);
     return L == LAYOUT_LPC ? mcmc_launch_lpc_eval(a, xin, lp, g, check, st)
                            : mcmc_launch_wpc_eval(a, xin, lp, g, check, st);
 }
 static hipError_t launch_step(Layout L, const KernelArgs& a, hipStream_t st) {
+    if (L == LAYOUT_GLM) return mcmc_launch_glm_step(a, st);
     return L == LAYOUT_LPC ? mcmc_launch_lpc_step(a, st) : mcmc_launch_wpc_step(a, st);
 }
 
 // [d][C] (stride ldc) <-> state layout
 static hipError_t cols_to_state(Layout L, double* state, int64_t ld, const double* cols, int64_t ldc, int d, int64_t C,
                                 hipStream_t st) {
-    if (L == LAYOUT_LPC) return mcmc_copy_cols(state, ld, cols, ldc, d, C, st);
+    if (L != LAYOUT_WPC) return mcmc_copy_cols(state, ld, cols, ldc, d, C, st);
     // [d][C] -> [C][ld]: transpose of a d x C matrix
     hipError_t e = hipMemsetAsync(state, 0, (size_t)C * ld * 8, st);
     if (e != hipSuccess) return e;
@@ -361,7 +394,7 @@ static hipError_t cols_to_state(Layout L, double* state, int64_t ld, const doubl
 }
 static hipError_t state_to_cols(Layout L, double* cols, int64_t ldc, const double* state, int64_t ld, int d, int64_t C,
                                 hipStream_t st) {
-    if (L == LAYOUT_LPC) return mcmc_copy_cols(cols, ldc, state, ld, d, C, st);
+    if (L != LAYOUT_WPC) return mcmc_copy_cols(cols, ldc, state, ld, d, C, st);
     return mcmc_transpose(cols, ldc, state, ld, 1, C, d, st);
 }
 
@@ -371,11 +404,10 @@ extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, 
     mcmc_ctx* ctx = m->ctx;
     if (int r = set_device(ctx)) return r;
     const int d = m->args.d;
-    if (!model_is_separable(m)) return fail(MCMC_E_UNSUPPORTED, "model kind has no eval kernel");
-    if (d > mcmc_wpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "d > 2048 is not built");
+    if (model_is_separable(m) && d > mcmc_wpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "d > 2048 is not built");
     const Layout L = layout_for(m);
     const int64_t ld = ld_for(L, nchains, d);
-    const size_t nst = L == LAYOUT_LPC ? (size_t)d * ld : (size_t)nchains * ld;
+    const size_t nst = L != LAYOUT_WPC ? (size_t)d * ld : (size_t)nchains * ld;
     double *dcols = nullptr, *dx = nullptr, *dlp = nullptr, *dg = nullptr;
     hipStream_t st = ctx->stream;
     int rc = MCMC_OK;
@@ -427,7 +459,7 @@ static int init_state(mcmc_chains* c) {
         HIP_TRY(mcmc_broadcast_rows(c->st.x, c->ld, m->d_init, d, c->C, st));
     }
     KernelArgs a = base_args(m, c->C, c->ld);
-    HIP_TRY(launch_eval(c->layout, a, c->st.x, c->st.lp, nullptr, 1, st));
+    HIP_TRY(launch_eval(c->layout, a, c->st.x, c->st.lp, c->st.g, 1, st));
     if (sa.kind == SK_MALA && sa.tuner) HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, sa.drift_step, st));
     if (sa.kind == SK_HMC && sa.tuner) {
         HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, sa.leap_step, st));
@@ -467,8 +499,8 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     mcmc_ctx* ctx = m->ctx;
     if (int r = set_device(ctx)) return r;
     const int d = m->args.d;
-    if (!model_is_separable(m) || d > mcmc_wpc_max_d())
-        return fail(MCMC_E_UNSUPPORTED, "this model x size combination is not built yet");
+    if (model_is_separable(m) && d > mcmc_wpc_max_d())
+        return fail(MCMC_E_UNSUPPORTED, "separable targets support d <= 2048");
     auto* c = new mcmc_chains();
     c->model = m;
     c->C = nchains;
@@ -497,9 +529,11 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
         mcmc_chains_destroy(c);
         return code;
     };
-    const size_t nst = c->layout == LAYOUT_LPC ? (size_t)d * c->ld : (size_t)nchains * c->ld;
+    const size_t nst = c->layout != LAYOUT_WPC ? (size_t)d * c->ld : (size_t)nchains * c->ld;
     const size_t nc = (size_t)round_up(nchains, 64);
     if (int r = dmalloc(&c->st.x, nst)) return bail(r);
+    if (c->layout == LAYOUT_GLM)                 // gradient at the state (regression targets are not separable)
+        if (int r = dmalloc(&c->st.g, nst)) return bail(r);
     if (int r = dmalloc(&c->st.lp, nc)) return bail(r);
     const bool tuned = sa.tuner && (sa.kind == SK_MALA || sa.kind == SK_HMC);
     if (tuned || sa.kind == SK_HMCDA)
@@ -656,7 +690,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     HIP_TRY(hipStreamSynchronize(st));
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventRecord(ctx->ev0, st));
-    if (want_bits && L == LAYOUT_WPC) HIP_TRY(hipMemsetAsync(d_bits, 0, (size_t)nkept * nw * 8, st));
+    if (want_bits && L != LAYOUT_LPC) HIP_TRY(hipMemsetAsync(d_bits, 0, (size_t)nkept * nw * 8, st));
     for (int64_t done = 0; done < r->len; done += spl) {
         const int64_t n = std::min(spl, r->len - done);
         s.step_begin = c->steps_done + done + 1;
@@ -743,5 +777,28 @@ extern "C" int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr, 
     dfree(dc);
     dfree(dk);
     dfree(dout);
+    return rc;
+}
+
+extern "C" int mcmc_debug_mfma_f64(mcmc_ctx* ctx, int nk, const double* A, const double* B, const double* C,
+                                   double* D) {
+    if (!ctx || !A || !B || !C || !D || nk <= 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    if (int r = set_device(ctx)) return r;
+    double *dA = nullptr, *dB = nullptr, *dC = nullptr, *dD = nullptr;
+    int rc = MCMC_OK;
+    do {
+        if ((rc = dmalloc(&dA, 64 * (size_t)nk))) break;
+        if ((rc = dmalloc(&dB, 64 * (size_t)nk))) break;
+        if ((rc = dmalloc(&dC, 256))) break;
+        if ((rc = dmalloc(&dD, 256))) break;
+        hipError_t e = hipMemcpy(dA, A, 512 * (size_t)nk, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dB, B, 512 * (size_t)nk, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dC, C, 2048, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = mcmc_mfma_probe(dA, dB, dC, dD, nk, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = hipMemcpy(D, dD, 2048, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("mfma probe: ") + hipGetErrorString(e));
+    } while (0);
+    dfree(dA); dfree(dB); dfree(dC); dfree(dD);
     return rc;
 }

@@ -1,0 +1,735 @@
+// glm.hip -- regression models on fp64 MFMA: logistic (examples/logistic_regression.jl:16-22)
+// and linear (examples/linear_regression.jl:14-20) log-targets with their gradients, fused into
+// the RWM / MALA / HMC / HMCDA step loops.
+//
+// Mapping.  A wave owns a tile of 16 chains; the dense contractions are
+//     eta[obs][chain] = X[obs][:] . beta[:][chain]        (v_mfma_f64_16x16x4_f64, K = coordinates)
+//     G[coord][chain] = X[:][coord] . r[:][chain]          (same instruction, K = observations)
+// per 16-observation tile of X staged in LDS and shared by the workgroup's waves.  Lane l holds
+// chain cl = l & 15 and quarter q = l >> 4; for d-slice s (d > 64 is split over NW = d_pad/64
+// waves) it owns coordinates k = s*DS + 16m + 4q + e (m < DS/16, e < 4), which are exactly the four
+// normals of Philox blocks k/4 -- so proposals, momenta, gradients and every per-coordinate term
+// stay lane-local.  The MFMA row <-> coordinate maps are permuted to make that so:
+//     eta k-slice kk (= 4m + e), row q      <-> coordinate 16m + 4q + e
+//     G tile T, row i (= 4r + q')           <-> coordinate 16T + 4q' + r
+// and the eta accumulator (obs q + 4r on lane (q, cl)) is, register for register, the B operand
+// of the G product (k-slice r): no data movement between the two MFMA chains.
+//
+// Arithmetic (restated by oracle/oracle.c orc_glm_eval): v_mfma_f64_16x16x4_f64 is a
+// sequential fma chain over its k (probed bitwise on gfx950, scripts/probe_mfma.py), so eta is an
+// fma chain over coordinates in (m, e, q) order per slice, slices added left to right; G is an fma
+// chain over observations; per-coordinate sums are lane partials in (m, e) order combined as
+// (q0 + q2) + (q1 + q3), then slices left to right.
+#include "../common.hpp"
+#include "../detmath.hpp"
+#include "../models.hpp"
+#include "../host/kernels_api.hpp"
+
+namespace mcmc {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// workgroup: max(4, NW) waves = (4 / NW) tiles of 16 chains, or one tile when NW = 8
+template <int NW>
+constexpr int glm_block() { return 64 * (NW > 4 ? NW : 4); }
+constexpr int kGlmMaxWaves = 8;
+// NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
+
+struct GlmShape {
+    int nw;          // waves per 16-chain tile (d-slices)
+    int tpw;         // tiles per workgroup = max(4, nw) / nw
+    int ds;          // coordinates per wave
+    int nm;          // ds / 16
+    int d_pad;
+    int lds_stride;  // X tile row stride in LDS (doubles)
+    int64_t n_pad;
+};
+
+struct GlmArgs {
+    StepArgs s;
+    SamplerArgs sa;
+    ModelArgs m;
+    ChainState st;
+    GlmShape g;
+};
+
+// lane position inside the workgroup
+struct GlmPos {
+    int lane, q, cl, wave, slice, tile;
+    int64_t c;
+    bool live;
+    int base;
+};
+
+__device__ __forceinline__ GlmPos glm_pos(const GlmArgs& a) {
+    GlmPos p;
+    p.lane = threadIdx.x & 63;
+    p.q = p.lane >> 4;
+    p.cl = p.lane & 15;
+    p.wave = threadIdx.x >> 6;
+    p.slice = p.wave % a.g.nw;
+    p.tile = p.wave / a.g.nw;
+    p.c = ((int64_t)blockIdx.x * a.g.tpw + p.tile) * 16 + p.cl;
+    p.live = p.c < a.s.C;
+    p.base = p.slice * a.g.ds;
+    return p;
+}
+
+__device__ __forceinline__ int own_coord(const GlmPos& p, int slot) {
+    return p.base + 16 * (slot >> 2) + 4 * p.q + (slot & 3);
+}
+
+// LDS carve-up (doubles): X tile [16][stride] | Y tile [16] | eta partials [4 waves][64][4] |
+// chain scalars [4 waves][16] | int scratch
+struct GlmLds {
+    double* X;
+    double* Y;
+    double* part;
+    double* scal;
+    int* iscr;
+};
+
+__device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
+    GlmLds L;
+    L.X = smem;
+    L.Y = L.X + 16 * a.g.lds_stride;
+    L.part = L.Y + 16;
+    L.scal = L.part + kGlmMaxWaves * 64 * 4;
+    L.iscr = (int*)(L.scal + kGlmMaxWaves * 16);
+    return L;
+}
+
+size_t glm_lds_bytes(const GlmShape& g) {
+    return (size_t)(16 * g.lds_stride + 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4) * 8;
+}
+
+// sum of a per-chain quantity held as 4 quarter partials per wave and NW slice partials:
+// (q0 + q2) + (q1 + q3), then slices left to right.  Contains a barrier when nw > 1:
+// every wave of the workgroup must reach it.
+__device__ __forceinline__ double glm_sum(const GlmArgs& a, const GlmPos& p, const GlmLds& L, double v) {
+    v = v + __shfl_xor(v, 32, 64);
+    v = v + __shfl_xor(v, 16, 64);
+    if (a.g.nw == 1) return v;
+    __syncthreads();
+    if (p.q == 0) L.scal[p.wave * 16 + p.cl] = v;
+    __syncthreads();
+    double t = L.scal[(p.tile * a.g.nw) * 16 + p.cl];
+    for (int s = 1; s < a.g.nw; ++s) t = t + L.scal[(p.tile * a.g.nw + s) * 16 + p.cl];
+    return t;
+}
+
+// workgroup-wide max of a per-chain integer (leapfrog counts): every wave must reach it.
+__device__ __forceinline__ int64_t glm_max(const GlmLds& L, int64_t v, bool live) {
+    __syncthreads();
+    if (threadIdx.x == 0) L.iscr[0] = 1;
+    __syncthreads();
+    if (live) atomicMax(&L.iscr[0], (int)v);
+    __syncthreads();
+    const int r = L.iscr[0];
+    __syncthreads();
+    return r;
+}
+
+// log-target and (GRAD) gradient of the regression model at the lane's coordinates x.
+// Every wave of the workgroup calls it the same number of times (barriers inside).
+// gout doubles as the MFMA accumulator of G = X^T r (G[T] covers slots 4T..4T+3).
+template <int NM, int NW, bool GRAD>
+__device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
+                                        const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
+    const ModelArgs& M = a.m;
+    const GlmShape& g = a.g;
+    const int d = M.d;
+    const int S = g.lds_stride;
+    const bool logistic = M.kind == MK_LOGISTIC;
+    const double sgn = M.link_sign;
+    const double sn = M.noise_sigma, s2n = sn * sn;
+    const double logsn = logistic ? 0.0 : det_log(sn);
+    if (GRAD) {
+#pragma unroll
+        for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    double lik_part = 0.0;
+    const int64_t ntiles = g.n_pad / 16;
+    for (int64_t t = 0; t < ntiles; ++t) {
+        // stage X rows 16t..16t+15 (contiguous, 16 * d_pad doubles) into padded LDS rows: all loads of
+        // the tile are issued before the barrier that retires the previous tile's readers
+        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)t * 16 * g.d_pad);
+        constexpr int kBlk = glm_block<NW>();
+        constexpr int kHalf = 16 * 8 * NM * NW;               // f64x2 per tile (d_pad = 16 NM NW)
+        constexpr int kPer = (kHalf + kBlk - 1) / kBlk;
+        constexpr int kRound = kPer < 8 ? kPer : 8;
+        constexpr int kLgHalfrow = __builtin_ctz(8 * NM * NW);
+        const double ytile = (threadIdx.x < 16) ? M.Y[t * 16 + threadIdx.x] : 0.0;
+        f64x2 buf[kRound];
+#pragma unroll
+        for (int j = 0; j < kRound; ++j) {
+            const int i = threadIdx.x + kBlk * j;
+            buf[j] = src[i < kHalf ? i : 0];                  // unconditional load: no exec branch
+        }
+        __syncthreads();                                      // previous tile's readers are done
+#pragma unroll
+        for (int j0 = 0; j0 < kPer; j0 += kRound) {
+            if (j0 > 0) {
+#pragma unroll
+                for (int j = 0; j < kRound; ++j) {
+                    const int i = threadIdx.x + kBlk * (j0 + j);
+                    buf[j] = src[i < kHalf ? i : 0];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kRound; ++j) {
+                const int i = threadIdx.x + kBlk * (j0 + j);
+                if (i < kHalf) {
+                    const int row = i >> kLgHalfrow, col = 2 * (i & ((1 << kLgHalfrow) - 1));
+                    *reinterpret_cast<f64x2*>(&L.X[row * S + col]) = buf[j];
+                }
+            }
+        }
+        if (threadIdx.x < 16) L.Y[threadIdx.x] = ytile;
+        __syncthreads();
+        // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e
+        f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
+        const double* xrow = L.X + p.cl * S + p.base + 4 * p.q;
+#pragma unroll
+        for (int slot = 0; slot < (4 * NM); ++slot) {
+            if (true) {
+                const double av = xrow[16 * (slot >> 2) + (slot & 3)];
+                eta = __builtin_amdgcn_mfma_f64_16x16x4f64(av, x[slot], eta, 0, 0, 0);
+            }
+        }
+        if (NW > 1) {
+            double* mine = L.part + (p.wave * 64 + p.lane) * 4;
+            mine[0] = eta[0]; mine[1] = eta[1]; mine[2] = eta[2]; mine[3] = eta[3];
+            __syncthreads();
+            const double* p0 = L.part + ((p.tile * NW) * 64 + p.lane) * 4;
+            eta = f64x4{p0[0], p0[1], p0[2], p0[3]};
+            for (int s = 1; s < NW; ++s) {
+                const double* ps = L.part + ((p.tile * NW + s) * 64 + p.lane) * 4;
+                eta[0] = eta[0] + ps[0]; eta[1] = eta[1] + ps[1];
+                eta[2] = eta[2] + ps[2]; eta[3] = eta[3] + ps[3];
+            }
+        }
+        // elementwise: obs 16t + q + 4r for chain cl
+        double rv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t obs = t * 16 + p.q + 4 * r;
+            const double y = L.Y[p.q + 4 * r];
+            double term, rr;
+            if (logistic) {
+                const double tt = det_exp(-(sgn * eta[r]));             // prob = 1/(1+exp(-X*vars))
+                const double u = 1.0 + tt;
+                const double pr = 1.0 / u;
+                term = (y >= 0.5) ? det_log(pr) : det_log(1.0 - pr);   // Y ~ Bernoulli(prob)
+                const double dprob = 1.0 / ((pr - 1.0) + y);            // MCMCDerivRules.jl:111
+                rr = sgn * ((dprob * tt) / (u * u));
+            } else {
+                const double resid = y - eta[r];                        // resid = Y - X*vars
+                const double z = resid / sn;
+                term = -0.5 * (z * z + kLog2Pi) - logsn;                // resid ~ Normal(0, sn)
+                rr = resid / s2n;
+            }
+            const bool in = obs < M.n;
+            if (in) lik_part = lik_part + term;
+            rv[r] = in ? rr : 0.0;
+        }
+        if (GRAD) {
+            // G tile T, k-slice kk': A[i][k] = X[obs 4kk'+q][coord base+16T+4(i&3)+(i>>2)], i = cl
+            const double* gcol = L.X + p.base + 4 * (p.cl & 3) + (p.cl >> 2);
+#pragma unroll
+            for (int T = 0; T < NM; ++T) {
+                if (true) {
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const double av = gcol[(4 * kk + p.q) * S + 16 * T];
+                        G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, rv[kk], G[T], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    // likelihood: quarter combine only (identical in every slice wave)
+    double lik = lik_part + __shfl_xor(lik_part, 32, 64);
+    lik = lik + __shfl_xor(lik, 16, 64);
+    // prior vars ~ Normal(0, sp) over own coordinates
+    const double sp = M.prior_sigma, s2p = sp * sp, logsp = det_log(sp);
+    double pp = 0.0;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot) {
+        const int k = own_coord(p, slot);
+        if (true && k < d) {
+            const double z = (x[slot] - 0.0) / sp;
+            pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
+        }
+    }
+    const double prior = glm_sum(a, p, L, pp);
+    double acc = 0.0 + prior;                                           // LLAcc(0.) + ...
+    bool bad = !(acc - acc == 0.0);
+    acc = acc + lik;
+    bad = bad || !(acc - acc == 0.0);
+    oos = bad;
+    if (bad) acc = -__builtin_inf();
+    if (GRAD) {
+#pragma unroll
+        for (int slot = 0; slot < (4 * NM); ++slot)
+            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - x[slot]) / s2p + G[slot >> 2][slot & 3];
+    }
+    return acc;
+}
+
+// ------------------------------------------------------------------ state access (layout [d][ld])
+// Lane pointer at coordinate base + 4q; slot (m, e) adds the wave-uniform offset (16m + e) * ld,
+// so the 32 slot addresses cost SGPRs, not VGPRs.
+template <class T>
+__device__ __forceinline__ T* glm_lane_ptr(const GlmPos& p, T* base, int64_t ld, int64_t c) {
+    return base + (size_t)(p.base + 4 * p.q) * (size_t)ld + (size_t)c;
+}
+__device__ __forceinline__ bool glm_valid(const GlmArgs& a, const GlmPos& p, int slot) {
+    return own_coord(p, slot) < a.s.d;
+}
+template <int NM>
+__device__ __forceinline__ void glm_load(const GlmArgs& a, const GlmPos& p, const double* src,
+                                         double (&v)[(4 * NM)]) {
+    const double* lp = glm_lane_ptr(p, src, a.s.ld, p.live ? p.c : 0);
+    const size_t ld = (size_t)a.s.ld;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot)
+        v[slot] = glm_valid(a, p, slot) ? lp[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
+}
+template <int NM>
+__device__ __forceinline__ void glm_store(const GlmArgs& a, const GlmPos& p, double* dst, int64_t ldd,
+                                          const double (&v)[(4 * NM)]) {
+    if (!p.live) return;
+    double* lp = glm_lane_ptr(p, dst, ldd, p.c);
+    const size_t ld = (size_t)ldd;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot)
+        if (glm_valid(a, p, slot)) lp[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] = v[slot];
+}
+template <int NM>
+__device__ __forceinline__ void glm_store_kept(const GlmArgs& a, const GlmPos& p, int64_t kk, double* base,
+                                               const double (&v)[(4 * NM)]) {
+    if (base == nullptr) return;
+    glm_store<NM>(a, p, base + (size_t)kk * (size_t)a.s.d * (size_t)a.s.C, a.s.C, v);
+}
+template <int NM>
+__device__ __forceinline__ void glm_load4(const GlmArgs& a, const GlmPos& p, const double* src,
+                                          f64x4 (&v)[NM]) {
+    const double* lp = glm_lane_ptr(p, src, a.s.ld, p.live ? p.c : 0);
+    const size_t ld = (size_t)a.s.ld;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot)
+        v[slot >> 2][slot & 3] = glm_valid(a, p, slot) ? lp[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
+}
+template <int NM>
+__device__ __forceinline__ void glm_store4(const GlmArgs& a, const GlmPos& p, double* dst, int64_t ldd,
+                                           const f64x4 (&v)[NM]) {
+    if (!p.live) return;
+    double* lp = glm_lane_ptr(p, dst, ldd, p.c);
+    const size_t ld = (size_t)ldd;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot)
+        if (glm_valid(a, p, slot)) lp[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] = v[slot >> 2][slot & 3];
+}
+template <int NM>
+__device__ __forceinline__ void glm_store_kept4(const GlmArgs& a, const GlmPos& p, int64_t kk, double* base,
+                                                const f64x4 (&v)[NM]) {
+    if (base == nullptr) return;
+    glm_store4<NM>(a, p, base + (size_t)kk * (size_t)a.s.d * (size_t)a.s.C, a.s.C, v);
+}
+__device__ __forceinline__ void glm_store_bit(const GlmArgs& a, const GlmPos& p, int64_t kk, bool acc) {
+    if (p.live && acc && p.q == 0 && p.slice == 0 && a.s.acc_bits != nullptr)
+        atomicOr((unsigned long long*)&a.s.acc_bits[(size_t)kk * (size_t)a.s.nw + (size_t)(p.c >> 6)],
+                 1ull << (p.c & 63));
+}
+
+// normals of the lane's coordinates; padded coordinates (k >= d) get 0 so they stay at 0
+template <int NM>
+__device__ __forceinline__ void glm_normals(const GlmPos& p, const Stream& rs, uint32_t chain, uint32_t step,
+                                            int d, double (&z)[(4 * NM)]) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        if (true) {
+            const uint32_t blk = (uint32_t)((p.base >> 2) + 4 * m + p.q);   // coords 4*blk .. 4*blk+3
+            const u32x4 w = rs.block(chain, step, blk, TAG_NORMAL);
+            normals4(w, z[4 * m], z[4 * m + 1], z[4 * m + 2], z[4 * m + 3]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if ((int)(4 * blk) + e >= d) z[4 * m + e] = 0.0;
+        } else {
+            z[4 * m] = z[4 * m + 1] = z[4 * m + 2] = z[4 * m + 3] = 0.0;
+        }
+    }
+}
+
+__device__ __forceinline__ bool glm_mh_short_circuit(const Stream& rs, uint32_t chain, uint32_t step, double ratio) {
+    bool acc = ratio > 0.0;                                           // RWM.jl:63, MALA.jl:108
+    if (!acc) {
+        const u32x4 w = rs.block(chain, step, 0u, TAG_ACCEPT);
+        acc = ratio > det_log(uniform53(w.x, w.y));
+    }
+    return acc;
+}
+
+__device__ __forceinline__ double glm_tune_factor(int32_t acc, int32_t prop, double target) {
+    const double rate = (double)acc / (double)prop;                   // MALA.jl:36-39, HMC.jl:165-169
+    return 1.0 / (1.0 + det_exp(-11.0 * (rate - target))) + 0.5;
+}
+
+// ------------------------------------------------------------------ kernels
+template <int NM, int NW>
+__global__ __launch_bounds__(glm_block<NW>()) void glm_eval_kernel(GlmArgs a, const double* xin, double* lp_out,
+                                                             double* g_out, int32_t check) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const GlmPos p = glm_pos(a);
+    const GlmLds L = glm_lds(a, smem);
+    double x[(4 * NM)];
+    f64x4 g[NM];
+    glm_load<NM>(a, p, xin, x);
+    bool oos;
+    const double lp = glm_eval<NM, NW, true>(a, p, L, x, g, oos);
+    if (p.live && p.q == 0 && p.slice == 0) lp_out[p.c] = lp;
+    if (g_out) glm_store4<NM>(a, p, g_out, a.s.ld, g);
+    if (check && p.live && !(lp - lp == 0.0)) atomicOr(a.s.err, 1);
+}
+
+template <int NM, int NW>
+__global__ __launch_bounds__(glm_block<NW>()) void glm_rwm(GlmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const StepArgs& s = a.s;
+    const GlmPos p = glm_pos(a);
+    const GlmLds L = glm_lds(a, smem);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    f64x4 dummy[NM];
+    const double* scl = s.scale + p.base + 4 * p.q;
+    double lp = a.st.lp[p.live ? p.c : 0];
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        double xp[(4 * NM)];
+        {
+            double x[(4 * NM)];
+            glm_load<NM>(a, p, a.st.x, x);
+            glm_normals<NM>(p, rs, chain, (uint32_t)i, a.s.d, xp);
+#pragma unroll
+            for (int slot = 0; slot < (4 * NM); ++slot)                         // RWM.jl:59
+                xp[slot] = x[slot] + xp[slot] * (glm_valid(a, p, slot) ? scl[16 * (slot >> 2) + (slot & 3)] : 0.0);
+        }
+        bool oos;
+        const double lpp = glm_eval<NM, NW, false>(a, p, L, xp, dummy, oos);
+        const bool acc = glm_mh_short_circuit(rs, chain, (uint32_t)i, lpp - lp);
+        if (acc) {
+            glm_store<NM>(a, p, a.st.x, s.ld, xp);
+            lp = lpp;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            if (!acc) glm_load<NM>(a, p, a.st.x, xp);
+            glm_store_kept<NM>(a, p, kk, s.samples, xp);
+            glm_store_bit(a, p, kk, acc);
+        }
+    }
+    if (p.live && p.q == 0 && p.slice == 0) a.st.lp[p.c] = lp;
+}
+
+template <int NM, int NW>
+__global__ __launch_bounds__(glm_block<NW>()) void glm_mala(GlmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const GlmPos p = glm_pos(a);
+    const GlmLds L = glm_lds(a, smem);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int64_t cc = p.live ? p.c : 0;
+    double lp = a.st.lp[cc];
+    double h = sa.tuner ? a.st.t_step[cc] : sa.drift_step;
+    int32_t n_acc = sa.tuner ? a.st.t_acc[cc] : 0;
+    int32_t n_prop = sa.tuner ? a.st.t_prop[cc] : 0;
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        if (sa.tuner) n_prop += 1;
+        const double half = h / 2.0;
+        const double sq = __builtin_sqrt(h);
+        const double twoh = 2.0 * h;
+        const double Lc = det_log(kTwoPi * h) / 2.0;
+        double xp[(4 * NM)];
+        f64x4 gp[NM];
+        double qf = 0.0;
+        {
+            double x[(4 * NM)];                                        // state, reloaded after eval
+            glm_normals<NM>(p, rs, chain, (uint32_t)i, a.s.d, xp);
+            glm_load<NM>(a, p, a.st.x, x);
+            glm_load4<NM>(a, p, a.st.g, gp);                           // current gradient (state)
+#pragma unroll
+            for (int slot = 0; slot < (4 * NM); ++slot) {
+                const double pm = x[slot] + half * gp[slot >> 2][slot & 3];   // MALA.jl:98
+                xp[slot] = pm + sq * xp[slot];                                 // MALA.jl:100
+                const double e = pm - xp[slot];
+                if (glm_valid(a, p, slot)) qf = qf + ((-(e * e)) / twoh - Lc);   // MALA.jl:103
+            }
+        }
+        qf = glm_sum(a, p, L, qf);
+        bool oos;
+        const double lpp = glm_eval<NM, NW, true>(a, p, L, xp, gp, oos);    // MALA.jl:101
+        double qb = 0.0;
+        {
+            double x[(4 * NM)];
+            glm_load<NM>(a, p, a.st.x, x);
+#pragma unroll
+            for (int slot = 0; slot < (4 * NM); ++slot) {
+                const double e = (xp[slot] + half * gp[slot >> 2][slot & 3]) - x[slot];   // MALA.jl:104-105
+                if (glm_valid(a, p, slot)) qb = qb + ((-(e * e)) / twoh - Lc);
+            }
+        }
+        qb = glm_sum(a, p, L, qb);
+        const double ratio = ((lpp + qb) - lp) - qf;                   // MALA.jl:107
+        const bool acc = glm_mh_short_circuit(rs, chain, (uint32_t)i, ratio);
+        if (acc) {
+            glm_store<NM>(a, p, a.st.x, s.ld, xp);
+            glm_store4<NM>(a, p, a.st.g, s.ld, gp);
+            lp = lpp;
+            if (sa.tuner) n_acc += 1;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            if (!acc) {
+                glm_load<NM>(a, p, a.st.x, xp);
+                glm_load4<NM>(a, p, a.st.g, gp);
+            }
+            glm_store_kept<NM>(a, p, kk, s.samples, xp);
+            glm_store_kept4<NM>(a, p, kk, s.grads, gp);
+            glm_store_bit(a, p, kk, acc);
+        }
+        if (sa.tuner && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // MALA.jl:116-118
+            h = h * glm_tune_factor(n_acc, n_prop, sa.target_rate);
+            n_acc = 0;
+            n_prop = 0;
+        }
+    }
+    if (p.live && p.q == 0 && p.slice == 0) {
+        a.st.lp[p.c] = lp;
+        if (sa.tuner) {
+            a.st.t_step[p.c] = h;
+            a.st.t_acc[p.c] = n_acc;
+            a.st.t_prop[p.c] = n_prop;
+        }
+    }
+}
+
+template <int NM, int NW, bool DA>
+__global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const GlmPos p = glm_pos(a);
+    const GlmLds L = glm_lds(a, smem);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int64_t cc = p.live ? p.c : 0;
+    const bool tuned = !DA && sa.tuner;
+    const int64_t max_leaps = sa.max_leaps;
+    double lp = a.st.lp[cc];
+    double eps = (DA || tuned) ? a.st.t_step[cc] : sa.leap_step;
+    int64_t nl_fixed = tuned ? (int64_t)a.st.t_leaps[cc] : sa.n_leaps;
+    double eps_bar = DA ? a.st.t_bar[cc] : 0.0;
+    double h_bar = DA ? a.st.t_h[cc] : 0.0;
+    int32_t n_acc = tuned ? a.st.t_acc[cc] : 0;
+    int32_t n_prop = tuned ? a.st.t_prop[cc] : 0;
+    const double mu = DA ? det_log(10.0) : 0.0;
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        if (tuned) n_prop += 1;
+        double x[(4 * NM)], m[(4 * NM)];
+        f64x4 g[NM];
+        glm_normals<NM>(p, rs, chain, (uint32_t)i, a.s.d, m);          // state0.m = randn(model.size)
+        double mm = 0.0;
+#pragma unroll
+        for (int slot = 0; slot < (4 * NM); ++slot)
+            if (glm_valid(a, p, slot)) mm = __builtin_fma(m[slot], m[slot], mm);
+        const double H0 = -lp + 0.5 * glm_sum(a, p, L, mm);         // update!(state0)
+        glm_load<NM>(a, p, a.st.x, x);
+        glm_load4<NM>(a, p, a.st.g, g);
+        int64_t nl;
+        if (DA) {
+            const double r = round_away(sa.len / eps);              // HMCDA.jl:104
+            nl = r < 1.0 ? 1 : (r > (double)max_leaps ? max_leaps : (int64_t)r);
+        } else {
+            nl = nl_fixed;
+        }
+        const int64_t nl_wg = (DA || tuned) ? glm_max(L, nl, p.live) : nl;
+        double lpl = lp;
+        for (int64_t l = 0; l < nl_wg; ++l) {
+            const bool active = l < nl;                              // chains that finished keep still
+            if (active) {
+#pragma unroll
+                for (int slot = 0; slot < (4 * NM); ++slot) {
+                    m[slot] = m[slot] + (0.5 * g[slot >> 2][slot & 3]) * eps;   // n.m += 0.5*n.grad*ve
+                    x[slot] = x[slot] + eps * m[slot];                          // n.pars += ve * n.m
+                }
+            }
+            bool oos;
+            lpl = glm_eval<NM, NW, true>(a, p, L, x, g, oos);                // calc!(n, ll); same x -> same (lp, g)
+            if (active) {
+#pragma unroll
+                for (int slot = 0; slot < (4 * NM); ++slot) m[slot] = m[slot] + (0.5 * g[slot >> 2][slot & 3]) * eps;
+            }
+        }
+        mm = 0.0;
+#pragma unroll
+        for (int slot = 0; slot < (4 * NM); ++slot)
+            if (glm_valid(a, p, slot)) mm = __builtin_fma(m[slot], m[slot], mm);
+        const double H = -lpl + 0.5 * glm_sum(a, p, L, mm);
+        const u32x4 w = rs.block(chain, (uint32_t)i, 0u, TAG_ACCEPT);
+        const double u = uniform53(w.x, w.y);
+        double pa = 0.0;
+        bool acc;
+        if (DA) {
+            pa = __builtin_fmin(1.0, det_exp(H0 - H));              // HMCDA.jl:120
+            acc = u < pa;
+        } else {
+            acc = u < det_exp(H0 - H);                              // HMC.jl:280
+        }
+        if (acc) {
+            glm_store<NM>(a, p, a.st.x, s.ld, x);
+            glm_store4<NM>(a, p, a.st.g, s.ld, g);
+            lp = lpl;
+            if (tuned) n_acc += 1;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            if (!acc) {
+                glm_load<NM>(a, p, a.st.x, x);
+                glm_load4<NM>(a, p, a.st.g, g);
+            }
+            glm_store_kept<NM>(a, p, kk, s.samples, x);
+            glm_store_kept4<NM>(a, p, kk, s.grads, g);
+            glm_store_bit(a, p, kk, acc);
+        }
+        if (DA) {
+            const double di = (double)i;
+            if (di < (double)s.tuner_burnin) {                      // HMCDA.jl:133-138
+                double eta = 1.0 / (di + sa.t0);
+                h_bar = (1.0 - eta) * h_bar + eta * (sa.rate - pa);
+                eps = det_exp(mu - (__builtin_sqrt(di) * h_bar) / sa.shrinkage);
+                eta = det_exp(det_log(di) * (-sa.step));
+                eps_bar = det_exp((1.0 - eta) * det_log(eps_bar) + eta * det_log(eps));
+            } else {
+                eps = eps_bar;
+            }
+        } else if (tuned && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {
+            eps = eps * glm_tune_factor(n_acc, n_prop, sa.target_rate);
+            double nlf = __builtin_ceil(sa.target_path / eps);
+            if (nlf > (double)sa.max_step) nlf = (double)sa.max_step;
+            if (nlf > (double)max_leaps) nlf = (double)max_leaps;
+            nl_fixed = (int64_t)nlf;
+            n_acc = 0;
+            n_prop = 0;
+        }
+    }
+    if (p.live && p.q == 0 && p.slice == 0) {
+        a.st.lp[p.c] = lp;
+        if (DA || tuned) a.st.t_step[p.c] = eps;
+        if (DA) {
+            a.st.t_bar[p.c] = eps_bar;
+            a.st.t_h[p.c] = h_bar;
+        } else if (tuned) {
+            a.st.t_leaps[p.c] = (int32_t)nl_fixed;
+            a.st.t_acc[p.c] = n_acc;
+            a.st.t_prop[p.c] = n_prop;
+        }
+    }
+}
+
+static GlmArgs glm_args(const KernelArgs& k, const GlmShape& g) {
+    GlmArgs a;
+    a.s = k.s;
+    a.sa = k.sa;
+    a.m = k.m;
+    a.st = k.st;
+    a.g = g;
+    return a;
+}
+
+static unsigned glm_grid(int64_t C, const GlmShape& g) {
+    const int64_t chains_per_wg = 16 * g.tpw;
+    return (unsigned)((C + chains_per_wg - 1) / chains_per_wg);
+}
+
+}  // namespace mcmc
+
+mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
+    // d <= 64: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two);
+    // 64 < d <= 512: NW = 2, 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW.
+    mcmc::GlmShape g{};
+    if (d <= 64) {
+        int nm = 1;
+        while (16 * nm < d) nm *= 2;
+        g.nw = 1;
+        g.nm = nm;
+    } else {
+        int nw = 2;
+        while (64 * nw < d) nw *= 2;
+        g.nw = nw;
+        g.nm = 4;
+    }
+    g.ds = 16 * g.nm;
+    g.d_pad = g.ds * g.nw;
+    g.tpw = (g.nw > 4 ? g.nw : 4) / g.nw;
+    g.lds_stride = g.d_pad + 2;
+    g.n_pad = (n + 15) / 16 * 16;
+    return g;
+}
+
+int mcmc_glm_max_d() { return 512; }
+
+template <int NM, int NW>
+static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
+    using namespace mcmc;
+    constexpr int B = glm_block<NW>();
+    switch (a.sa.kind) {
+        case SK_RWM: glm_rwm<NM, NW><<<grid, B, lds, st>>>(a); break;
+        case SK_MALA: glm_mala<NM, NW><<<grid, B, lds, st>>>(a); break;
+        case SK_HMC: glm_hmc<NM, NW, false><<<grid, B, lds, st>>>(a); break;
+        case SK_HMCDA: glm_hmc<NM, NW, true><<<grid, B, lds, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& k, hipStream_t st) {
+    using namespace mcmc;
+    const GlmShape g = mcmc_glm_shape(k.s.d, k.m.n);
+    const GlmArgs a = glm_args(k, g);
+    const size_t lds = glm_lds_bytes(g);
+    const dim3 grid(glm_grid(k.s.C, g));
+    switch (g.nm * 10 + g.nw) {
+        case 11: return glm_step_nm<1, 1>(a, lds, grid, st);
+        case 21: return glm_step_nm<2, 1>(a, lds, grid, st);
+        case 41: return glm_step_nm<4, 1>(a, lds, grid, st);
+        case 42: return glm_step_nm<4, 2>(a, lds, grid, st);
+        case 44: return glm_step_nm<4, 4>(a, lds, grid, st);
+        case 48: return glm_step_nm<4, 8>(a, lds, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& k, const double* xin, double* lp, double* g, int check,
+                                hipStream_t st) {
+    using namespace mcmc;
+    const GlmShape gs = mcmc_glm_shape(k.s.d, k.m.n);
+    const GlmArgs a = glm_args(k, gs);
+    const dim3 grid(glm_grid(k.s.C, gs));
+    const size_t lds = glm_lds_bytes(gs);
+    switch (gs.nm * 10 + gs.nw) {
+        case 11: glm_eval_kernel<1, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 21: glm_eval_kernel<2, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 41: glm_eval_kernel<4, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 42: glm_eval_kernel<4, 2><<<grid, glm_block<2>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 44: glm_eval_kernel<4, 4><<<grid, glm_block<4>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 48: glm_eval_kernel<4, 8><<<grid, glm_block<8>(), lds, st>>>(a, xin, lp, g, check); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}

@@ -87,6 +87,22 @@ __global__ void k_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, ui
     out[4 * i] = w.x; out[4 * i + 1] = w.y; out[4 * i + 2] = w.z; out[4 * i + 3] = w.w;
 }
 
+// v_mfma_f64_16x16x4_f64 probe: D = A[16x4] * B[4x16] + C, with the lane maps of
+// cdna_hip_programming.md §3 (A/B as the f32 16x16x4 form; C/D col = l&15, row = (l>>4) + 4*reg).
+// nk MFMAs chained over K = 4*nk: A [16][4nk], B [4nk][16], C/D [16][16] row-major.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__global__ void k_mfma_probe(const double* A, const double* B, const double* C, double* D, int nk) {
+    const int l = threadIdx.x;
+    f64x4 acc;
+    for (int r = 0; r < 4; ++r) acc[r] = C[((l >> 4) + 4 * r) * 16 + (l & 15)];
+    for (int kk = 0; kk < nk; ++kk) {
+        const double a = A[(l & 15) * (4 * nk) + 4 * kk + (l >> 4)];
+        const double b = B[(4 * kk + (l >> 4)) * 16 + (l & 15)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    for (int r = 0; r < 4; ++r) D[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
+}
+
 }  // namespace mcmc
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
@@ -132,5 +148,9 @@ hipError_t mcmc_detmath(int op, int64_t n, const double* x, const double* y, dou
 }
 hipError_t mcmc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out, hipStream_t st) {
     mcmc::k_philox<<<nblk(n, 256), 256, 0, st>>>(n, ctr, key, out);
+    return hipGetLastError();
+}
+hipError_t mcmc_mfma_probe(const double* A, const double* B, const double* C, double* D, int nk, hipStream_t st) {
+    mcmc::k_mfma_probe<<<1, 64, 0, st>>>(A, B, C, D, nk);
     return hipGetLastError();
 }

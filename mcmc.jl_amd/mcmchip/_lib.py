@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_sampler_validate", "mcmc_runner_validate",
     "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients",
-    "mcmc_run_serialmc", "mcmc_debug_detmath", "mcmc_debug_philox",
+    "mcmc_run_serialmc", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
 )
 
 
@@ -125,6 +125,7 @@ def load() -> ct.CDLL:
         "mcmc_debug_detmath": (ct.c_int, [P, ct.c_int, i64, dp, dp, dp]),
         "mcmc_debug_philox": (ct.c_int, [P, i64, ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32),
                                          ct.POINTER(ct.c_uint32)]),
+        "mcmc_debug_mfma_f64": (ct.c_int, [P, ct.c_int, dp, dp, dp, dp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

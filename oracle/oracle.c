@@ -86,7 +86,18 @@ static double orc_butterfly(double p[64]) {
     return p[0];
 }
 
-static double orc_dot(const double* v, int d, int order) {
+typedef struct { int d_pad, nw, ds; int64_t n_pad; } orc_glm_geo;
+static orc_glm_geo orc_glm_geometry(const orc_model* m);
+static double orc_glm_sum(const double* t, const orc_glm_geo* g, int d, int fused_sq);
+
+static int orc_is_glm(const orc_model* m) { return m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR; }
+
+static double orc_dot(const double* v, const orc_model* mdl, int order) {
+    const int d = mdl->d;
+    if (orc_is_glm(mdl)) {
+        orc_glm_geo geo = orc_glm_geometry(mdl);
+        return orc_glm_sum(v, &geo, d, 1);
+    }
     if (order == 0) {
         double a = 0.0;
         for (int j = 0; j < d; ++j) a = fma(v[j], v[j], a);
@@ -102,7 +113,12 @@ static double orc_dot(const double* v, int d, int order) {
     return orc_butterfly(p);
 }
 
-static double orc_sum(const double* t, int d, int order) {
+static double orc_sum(const double* t, const orc_model* mdl, int order) {
+    const int d = mdl->d;
+    if (orc_is_glm(mdl)) {
+        orc_glm_geo geo = orc_glm_geometry(mdl);
+        return orc_glm_sum(t, &geo, d, 0);
+    }
     if (order == 0) {
         double a = 0.0;
         for (int j = 0; j < d; ++j) a = a + t[j];
@@ -118,13 +134,129 @@ static double orc_sum(const double* t, int d, int order) {
     return orc_butterfly(p);
 }
 
+/* ------------------------------------------------------------ regression models (MFMA kernels) */
+/* Geometry of the regression kernels (glm.hip): d <= 64: one wave per 16-chain tile with
+   DS = d_pad = 16 NM (NM a power of two); d > 64: NW = 2, 4, 8 waves of DS = 64 coordinates,
+   d_pad = 64 NW; n_pad = round_up(n,16).  Lane quarter q of the wave for slice s owns coordinates
+   k = s*DS + 16m + 4q + e (m < DS/16, e < 4). */
+static orc_glm_geo orc_glm_geometry(const orc_model* m) {
+    orc_glm_geo g;
+    int nm = 1, nw = 1;
+    if (m->d <= 64) {
+        while (16 * nm < m->d) nm *= 2;
+    } else {
+        nm = 4;
+        nw = 2;
+        while (64 * nw < m->d) nw *= 2;
+    }
+    g.ds = 16 * nm;
+    g.nw = nw;
+    g.d_pad = g.ds * nw;
+    g.n_pad = (m->n + 15) / 16 * 16;
+    return g;
+}
+
+/* sum of per-coordinate terms t[k] (k < d_pad, zero beyond d) in the regression kernels' order:
+   lane partials in (m, e) order, quarter combine (p0+p2)+(p1+p3), slices combined left to right */
+static double orc_glm_sum(const double* t, const orc_glm_geo* g, int d, int fused_sq) {
+    double total = 0.0;
+    for (int s = 0; s < g->nw; ++s) {
+        double p[4];
+        for (int q = 0; q < 4; ++q) {
+            double a = 0.0;
+            for (int mm = 0; mm < g->ds / 16; ++mm)
+                for (int e = 0; e < 4; ++e) {
+                    int k = s * g->ds + 16 * mm + 4 * q + e;
+                    if (k < d) a = fused_sq ? fma(t[k], t[k], a) : a + t[k];
+                }
+            p[q] = a;
+        }
+        double w = (p[0] + p[2]) + (p[1] + p[3]);
+        total = s == 0 ? w : total + w;
+    }
+    return total;
+}
+
+/* lp and gradient of the logistic / linear models (examples/logistic_regression.jl:16-22,
+   examples/linear_regression.jl:14-20) with the DSL semantics (LLAcc: a non-finite running sum
+   after either `~` statement gives (-Inf, zeros); modelparser.jl:64-72).  x: [d]. */
+static double orc_glm_eval(const orc_model* m, const double* x, double* g, double* tmp) {
+    const int d = m->d;
+    const orc_glm_geo geo = orc_glm_geometry(m);
+    const int dp = geo.d_pad;
+    double* xp = tmp;                 /* [d_pad] */
+    double* G = tmp + dp;             /* [d_pad] */
+    double* t = tmp + 2 * dp;         /* [d_pad] */
+    for (int k = 0; k < dp; ++k) { xp[k] = k < d ? x[k] : 0.0; G[k] = 0.0; }
+    const double sp = m->prior_sigma, s2p = sp * sp, logsp = orc_log(sp);
+    const double sn = m->noise_sigma, s2n = sn * sn, logsn = orc_log(sn);
+    const double sgn = m->link_sign;
+    /* likelihood: lane (chain, q) accumulates obs 16t + q + 4r in (t, r) order */
+    double lik_part[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t i = 0; i < geo.n_pad; ++i) {
+        const double* Xi = (i < m->n) ? m->X + (size_t)i * d : NULL;
+        /* eta_i: per slice an fma chain over (mm, e, q), slices added left to right */
+        double eta = 0.0;
+        for (int s = 0; s < geo.nw; ++s) {
+            double a = 0.0;
+            for (int mm = 0; mm < geo.ds / 16; ++mm)
+                for (int e = 0; e < 4; ++e)
+                    for (int q = 0; q < 4; ++q) {
+                        int k = s * geo.ds + 16 * mm + 4 * q + e;
+                        double xik = (Xi && k < d) ? Xi[k] : 0.0;
+                        a = fma(xik, xp[k], a);
+                    }
+            eta = s == 0 ? a : eta + a;
+        }
+        double term = 0.0, r = 0.0;
+        if (i < m->n) {
+            const double y = m->Y[i];
+            if (m->kind == ORC_MODEL_LINEAR) {
+                double resid = y - eta;                           /* resid = Y - X*vars */
+                double z = resid / sn;
+                term = -0.5 * (z * z + ORC_LOG2PI) - logsn;       /* resid ~ Normal(0, sn) */
+                r = resid / s2n;                                  /* -d/dresid, MCMCDerivRules.jl:57 */
+            } else {
+                double tt = orc_exp(-(sgn * eta));                /* prob = 1/(1+exp(-X*vars)) */
+                double u = 1.0 + tt;
+                double p = 1.0 / u;
+                term = (y >= 0.5) ? orc_log(p) : orc_log(1.0 - p);   /* Y ~ Bernoulli(prob) */
+                double dprob = 1.0 / ((p - 1.0) + y);              /* dd1 += 1/(d.p1 - 1 + x) (MCMCDerivRules.jl:111) */
+                r = sgn * ((dprob * tt) / (u * u));                /* dprob/deta = s t / u^2 */
+            }
+            const int q = (int)(i & 3);
+            lik_part[q] = lik_part[q] + term;
+        }
+        /* G_k = sum_i X[i][k] r_i, fma chain over obs (padded obs: X = 0, r = 0) */
+        for (int k = 0; k < dp; ++k) {
+            double xik = (Xi && k < d) ? Xi[k] : 0.0;
+            G[k] = fma(xik, r, G[k]);
+        }
+    }
+    const double lik = (lik_part[0] + lik_part[2]) + (lik_part[1] + lik_part[3]);
+    for (int k = 0; k < dp; ++k) {
+        double z = (xp[k] - 0.0) / sp;
+        t[k] = -0.5 * (z * z + ORC_LOG2PI) - logsp;                /* vars ~ Normal(0, sp) */
+    }
+    const double prior = orc_glm_sum(t, &geo, d, 0);
+    double a = 0.0 + prior;
+    int oos = !isfinite(a);
+    a = a + lik;
+    oos = oos || !isfinite(a);
+    if (oos) a = -INFINITY;
+    if (g)
+        for (int k = 0; k < d; ++k) g[k] = oos ? 0.0 : (0.0 - xp[k]) / s2p + G[k];
+    return a;
+}
+
 /* ------------------------------------------------------------ models */
-/* Returns lp; writes the gradient into g (length d) when g != NULL; tmp: d doubles of scratch. */
+/* Returns lp; writes the gradient into g (length d) when g != NULL; tmp: scratch (see orc_scratch). */
 static double orc_eval(const orc_model* m, const double* x, double* g, double* tmp, int order) {
     const int d = m->d;
+    if (m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR) return orc_glm_eval(m, x, g, tmp);
     if (m->kind == ORC_MODEL_ISO) {
         /* model(v -> -dot(v,v), grad = v -> -2v)  README.md:60,63; test/test_syntax.jl:40-41 */
-        double lp = -orc_dot(x, d, order);
+        double lp = -orc_dot(x, m, order);
         if (g)
             for (int j = 0; j < d; ++j) g[j] = -2.0 * x[j];
         return lp;
@@ -137,7 +269,7 @@ static double orc_eval(const orc_model* m, const double* x, double* g, double* t
             double z = (x[j] - m->mu) / m->sigma;
             tmp[j] = -0.5 * (z * z + ORC_LOG2PI) - logsig;
         }
-        double lp = orc_sum(tmp, d, order);
+        double lp = orc_sum(tmp, m, order);
         int oos = !isfinite(lp);
         if (oos) lp = -INFINITY;                  /* OutOfSupportError -> (-Inf, zero(beta)), modelparser.jl:64-72 */
         if (g) {
@@ -212,8 +344,8 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
     double* xp = g + d;       /* proposal    */
     double* gp = xp + d;
     double* mom = gp + d;
-    double* tmp = mom + d;
-    double* sc = tmp + d;     /* RWM scale = model.scale .* sampler.scale (RWM.jl:52) */
+    double* sc = mom + d;     /* RWM scale = model.scale .* sampler.scale (RWM.jl:52) */
+    double* tmp = sc + d;     /* model scratch (orc_scratch) */
     for (int j = 0; j < d; ++j) x[j] = st->x[(size_t)j * C + c];
     for (int j = 0; j < d; ++j) sc[j] = m->scale ? m->scale[j] * s->scale : s->scale;
     double lp = st->lp[c];
@@ -259,13 +391,13 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 double e = pm - xp[j];
                 tmp[j] = (-(e * e)) / twoh - L;
             }
-            double qf = orc_sum(tmp, d, order);                               /* probNewGivenOld */
+            double qf = orc_sum(tmp, m, order);                               /* probNewGivenOld */
             double lpp = orc_eval(m, xp, gp, tmp, order);                     /* evalallg(proposedPars) */
             for (int j = 0; j < d; ++j) {
                 double e = (xp[j] + half * gp[j]) - x[j];
                 tmp[j] = (-(e * e)) / twoh - L;
             }
-            double qb = orc_sum(tmp, d, order);                               /* probOldGivenNew */
+            double qb = orc_sum(tmp, m, order);                               /* probOldGivenNew */
             double ratio = ((lpp + qb) - lp) - qf;
             acc = orc_mh_short_circuit(seed, chain, (uint32_t)i, ratio);
             if (acc) {
@@ -279,7 +411,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
             const int da = s->kind == ORC_HMCDA;
             if (!da && tuned) n_prop += 1;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* state0.m = randn(model.size) */
-            const double H0 = -lp + 0.5 * orc_dot(mom, d, order);             /* update!(state0) */
+            const double H0 = -lp + 0.5 * orc_dot(mom, m, order);             /* update!(state0) */
             memcpy(xp, x, sizeof(double) * d);
             memcpy(gp, g, sizeof(double) * d);
             int64_t nl;
@@ -290,7 +422,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 nl = nl_fixed;
             }
             double lpl = orc_trajectory(m, eps, nl, xp, mom, gp, lp, tmp, order);
-            const double H = -lpl + 0.5 * orc_dot(mom, d, order);
+            const double H = -lpl + 0.5 * orc_dot(mom, m, order);
             const double u = orc_accept_uniform(seed, chain, (uint32_t)i);
             if (da) {
                 p_da = fmin(1.0, orc_exp(H0 - H));                            /* min(1, exp(H0-H)), NaN-ignoring */
@@ -354,13 +486,18 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
 }
 
 /* ------------------------------------------------------------ exported API (ctypes) */
+static size_t orc_scratch(const orc_model* m) {
+    size_t n = (size_t)m->d + 16;
+    if (orc_is_glm(m)) n = 3 * (size_t)orc_glm_geometry(m).d_pad + 16;
+    return n;
+}
 
 /* SamplerTask initialisation: lp = eval(x), tuner state defaults.  Returns the number of
    chains whose start is out of support ("Initial values out of model support", RWM.jl:55). */
 int64_t orc_init(const orc_model* m, const orc_sampler* s, int64_t C, orc_state* st, int order) {
     const int d = m->d;
     int64_t bad = 0;
-    double* buf = (double*)malloc(sizeof(double) * 2 * (size_t)(d > 0 ? d : 1));
+    double* buf = (double*)malloc(sizeof(double) * ((size_t)d + orc_scratch(m)));
     double* x = buf;
     double* tmp = buf + d;
     for (int64_t c = 0; c < C; ++c) {
@@ -388,7 +525,7 @@ void orc_run(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t ch
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
 #endif
     {
-        double* buf = (double*)malloc(sizeof(double) * 7 * (size_t)d);
+        double* buf = (double*)malloc(sizeof(double) * (6 * (size_t)d + orc_scratch(m)));
 #ifdef _OPENMP
 #pragma omp for schedule(static)
 #endif
@@ -403,7 +540,7 @@ void orc_run(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t ch
 /* model.eval / evalallg on a batch x[d][C] */
 void orc_eval_batch(const orc_model* m, int64_t C, const double* xs, double* lp, double* grad, int order) {
     const int d = m->d;
-    double* buf = (double*)malloc(sizeof(double) * 3 * (size_t)d);
+    double* buf = (double*)malloc(sizeof(double) * (2 * (size_t)d + orc_scratch(m)));
     for (int64_t c = 0; c < C; ++c) {
         for (int j = 0; j < d; ++j) buf[j] = xs[(size_t)j * C + c];
         lp[c] = orc_eval(m, buf, buf + d, buf + 2 * d, order);

@@ -219,3 +219,78 @@ def test_divergent_hmc_rejects(gpu, d):
     s, g, acc = oc.run(r)
     assert_parity(ch, s, g, acc, "hmc")
     assert not ch.diagnostics["accept"].any()
+
+
+# ------------------------------------------------------------------ regression models (fp64 MFMA)
+def _glm_model(kind, d, n=50, seed=0):
+    rng = np.random.default_rng(seed + d)
+    X = np.hstack([np.ones((n, 1)), rng.normal(size=(n, d - 1))])
+    beta0 = rng.normal(size=d) * 0.3
+    if kind == "logistic":
+        Y = (rng.random(n) < 1 / (1 + np.exp(-X @ beta0))).astype(float)
+        return mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(d), gradient=True)
+    Y = X @ beta0 + rng.normal(size=n)
+    return mc.model(mc.LinearRegression(X, Y, prior_sigma=1.0, noise_sigma=1.0), vars=np.zeros(d), gradient=True)
+
+
+GLM_SAMPLERS = {
+    "rwm": lambda: mc.RWM(0.05),
+    "mala": lambda: mc.MALA(0.002),
+    "mala_tuned": lambda: mc.MALA(0.01, mc.EmpMCTuner(0.6, adaptStep=3)),
+    "hmc": lambda: mc.HMC(3, 0.02),
+    "hmc_tuned": lambda: mc.HMC(2, 0.05, mc.EmpMCTuner(0.7, adaptStep=3, maxStep=6)),
+    "hmcda": lambda: mc.HMCDA(len=0.1),
+}
+
+
+@pytest.mark.parametrize("sname", list(GLM_SAMPLERS))
+@pytest.mark.parametrize("kind", ["logistic", "linear"])
+@pytest.mark.parametrize("d", [3, 16, 37, 64, 100, 200, 300])
+def test_glm_sampler_parity(gpu, sname, kind, d):
+    m = _glm_model(kind, d)
+    C = 40                                               # not a multiple of 16: tail tile
+    r = mc.SerialMC(steps=14, burnin=4, thinning=2)
+    chain = mc.run((m * GLM_SAMPLERS[sname]() * r).batch(C, seed=99 + d))
+    oc = orc.OracleChains(m, GLM_SAMPLERS[sname](), nchains=C, seed=99 + d)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, sname)
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+
+
+@pytest.mark.parametrize("kind", ["logistic", "linear"])
+@pytest.mark.parametrize("d", [10, 130])
+def test_glm_eval_matches_oracle(gpu, kind, d):
+    m = _glm_model(kind, d, n=70)
+    x = np.random.default_rng(3).normal(size=(d, 37)) * 0.2
+    lp, g = m.evalallg(x)
+    lp_r, g_r = orc.eval_batch(m, x)
+    assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
+
+
+def test_glm_continue_and_shard(gpu):
+    m = _glm_model("logistic", 20)
+    r = mc.SerialMC(steps=10, burnin=3)
+    t = (m * mc.MALA(0.01, mc.EmpMCTuner(0.5, adaptStep=2)) * r).batch(50, seed=5)
+    c1, c2 = mc.run(t), None
+    c2 = mc.run(c1)
+    oc = orc.OracleChains(m, mc.MALA(0.01, mc.EmpMCTuner(0.5, adaptStep=2)), nchains=50, seed=5)
+    s1, g1, a1 = oc.run(r)
+    s2, g2, a2 = oc.run(r)
+    assert_parity(c1, s1, g1, a1, "mala")
+    assert_parity(c2, s2, g2, a2, "mala")
+    lo = mc.run((m * mc.HMC(2, 0.05) * r).batch(23, seed=5, chain_offset=0))
+    hi = mc.run((m * mc.HMC(2, 0.05) * r).batch(27, seed=5, chain_offset=23))
+    full = mc.run((m * mc.HMC(2, 0.05) * r).batch(50, seed=5))
+    assert np.array_equal(np.concatenate([lo._samples, hi._samples], axis=2), full._samples)
+
+
+def test_logistic_out_of_support_rejects(gpu):
+    """Huge proposals push prob to exactly 0/1: log(0) -> LLAcc throws -> (-Inf, 0) -> reject."""
+    X = np.hstack([np.ones((30, 1)), np.random.default_rng(1).normal(size=(30, 3)) * 30])
+    Y = (np.random.default_rng(2).random(30) < 0.5).astype(float)
+    m = mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(4), gradient=True)
+    r = mc.SerialMC(steps=8)
+    ch = mc.run((m * mc.RWM(50.0) * r).batch(20, seed=1))
+    oc = orc.OracleChains(m, mc.RWM(50.0), nchains=20, seed=1)
+    s, g, acc = oc.run(r)
+    assert_parity(ch, s, g, acc, "rwm")

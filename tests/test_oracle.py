@@ -270,3 +270,101 @@ def test_init_out_of_support_raises():
     m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.zeros(2), gradient=True)
     with pytest.raises(AssertionError, match="out of model support"):
         orc.OracleChains(m, mc.RWM(0.1), nchains=2, init_x=np.array([[np.inf, 0.0], [0.0, 0.0]]))
+
+
+# ------------------------------------------------------------------ regression models
+def _logistic_data(n, d, seed=0, sign=1.0):
+    """examples/logistic_regression.jl:10-13 with the build's synthetic generator (numpy here)."""
+    rng = np.random.default_rng(seed)
+    X = np.hstack([np.ones((n, 1)), rng.normal(size=(n, d - 1))])
+    beta0 = rng.normal(size=d)
+    Y = (rng.random(n) < 1 / (1 + np.exp(-sign * (X @ beta0)))).astype(float)
+    return X, Y
+
+
+def _linear_data(n, d, seed=0):
+    rng = np.random.default_rng(seed)
+    X = np.hstack([np.ones((n, 1)), rng.normal(size=(n, d - 1))])
+    beta0 = rng.normal(size=d)
+    return X, X @ beta0 + rng.normal(size=n)
+
+
+@pytest.mark.parametrize("d", [10, 37, 130, 300])
+def test_logistic_eval_matches_closed_form(d):
+    X, Y = _logistic_data(200, d, seed=d)
+    m = mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(d), gradient=True)
+    B = np.random.default_rng(1).normal(size=(d, 5)) * 0.1
+    lp, g = orc.eval_batch(m, B)
+    eta = X @ B
+    p = 1 / (1 + np.exp(-eta))
+    ll = (Y[:, None] * np.log(p) + (1 - Y[:, None]) * np.log(1 - p)).sum(0)
+    prior = stats.norm.logpdf(B).sum(0)
+    np.testing.assert_allclose(lp, ll + prior, rtol=1e-12)
+    np.testing.assert_allclose(g, -B + X.T @ (Y[:, None] - p), rtol=1e-9, atol=1e-11)
+
+
+def test_logistic_link_sign_variant():
+    """test/test_syntax.jl:13,18 writes prob = 1/(1+exp(X*vars))."""
+    X, Y = _logistic_data(100, 6, seed=3, sign=-1.0)
+    m = mc.model(mc.LogisticRegression(X, Y, link_sign=-1.0), vars=np.zeros(6), gradient=True)
+    B = np.random.default_rng(2).normal(size=(6, 3)) * 0.2
+    lp, g = orc.eval_batch(m, B)
+    p = 1 / (1 + np.exp(X @ B))
+    ll = (Y[:, None] * np.log(p) + (1 - Y[:, None]) * np.log(1 - p)).sum(0)
+    np.testing.assert_allclose(lp, ll + stats.norm.logpdf(B).sum(0), rtol=1e-12)
+    np.testing.assert_allclose(g, -B - X.T @ (Y[:, None] - p), rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("d", [10, 200])
+def test_linear_eval_matches_closed_form(d):
+    X, Y = _linear_data(150, d, seed=d)
+    m = mc.model(mc.LinearRegression(X, Y, prior_sigma=1.5, noise_sigma=0.7), vars=np.zeros(d), gradient=True)
+    B = np.random.default_rng(4).normal(size=(d, 4)) * 0.1
+    lp, g = orc.eval_batch(m, B)
+    R = Y[:, None] - X @ B
+    np.testing.assert_allclose(lp, stats.norm(0, 0.7).logpdf(R).sum(0) + stats.norm(0, 1.5).logpdf(B).sum(0),
+                               rtol=1e-12)
+    np.testing.assert_allclose(g, -B / 1.5**2 + X.T @ R / 0.7**2, rtol=1e-9, atol=1e-10)
+
+
+def test_glm_gradient_finite_difference():
+    """helper_diff.jl:8-37 on the Bernoulli and Normal-residual rules (test_diff.jl:14,47)."""
+    for kind in ("logistic", "linear"):
+        d = 6
+        X, Y = _logistic_data(80, d) if kind == "logistic" else _linear_data(80, d)
+        tgt = mc.LogisticRegression(X, Y) if kind == "logistic" else mc.LinearRegression(X, Y)
+        m = mc.model(tgt, vars=np.zeros(d), gradient=True)
+        x0 = np.random.default_rng(5).normal(size=(d, 1)) * 0.3
+        lp0, g0 = orc.eval_batch(m, x0)
+        for j in range(d):
+            x1 = x0.copy()
+            x1[j] += 1e-7
+            gn = (orc.eval_batch(m, x1)[0] - lp0) / 1e-7
+            assert abs(g0[j, 0] - gn[0]) / max(2e-2, abs(g0[j, 0])) < 2e-2
+
+
+def test_logistic_out_of_support():
+    """p rounds to 1 with Y = 0: log(1-p) = -Inf -> LLAcc throws -> (-Inf, zeros)."""
+    X = np.array([[1.0, 50.0], [1.0, -1.0]])
+    Y = np.array([0.0, 1.0])
+    m = mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(2), gradient=True)
+    lp, g = orc.eval_batch(m, np.array([[0.0], [1.0]]))
+    assert lp[0] == -np.inf and (g == 0).all()
+
+
+def test_mala_logistic_recovers_posterior_mean():
+    X, Y = _logistic_data(400, 4, seed=9)
+    m = mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(4), gradient=True)
+    oc = orc.OracleChains(m, mc.MALA(0.02), nchains=8, seed=3)
+    s, _, acc = oc.run(mc.SerialMC(steps=3000, burnin=1000, thinning=5))
+    post = s.mean(axis=(0, 2))
+    # Laplace approximation of the posterior mean by Newton's method
+    b = np.zeros(4)
+    for _ in range(50):
+        p = 1 / (1 + np.exp(-X @ b))
+        gr = X.T @ (Y - p) - b
+        H = -(X.T * (p * (1 - p))) @ X - np.eye(4)
+        b = b - np.linalg.solve(H, gr)
+    sd = np.sqrt(np.diag(np.linalg.inv(-H)))
+    assert np.all(np.abs(post - b) < 0.25 * sd + 0.02)
+    assert 0.2 < acc.mean() < 0.99
