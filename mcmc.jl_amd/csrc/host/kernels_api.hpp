@@ -29,6 +29,8 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_glm_max_d();
+// padded covariate row length the regression kernels read (X_pad is [n_pad][d_pad])
+int mcmc_glm_d_pad(int d);
 
 hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st);
 hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st);

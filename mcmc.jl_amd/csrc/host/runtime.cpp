@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -64,6 +65,8 @@ struct mcmc_model {
     double* d_scale = nullptr;
     double* d_X = nullptr;
     double* d_Y = nullptr;
+    int chains_alive = 0;            // chains created on this model and not yet destroyed
+    bool released = false;           // mcmc_model_destroy called: free when the last chains go
 };
 
 enum Layout { LAYOUT_LPC = 0, LAYOUT_WPC = 1, LAYOUT_GLM = 2 };
@@ -87,6 +90,22 @@ struct mcmc_chains {
     int store_grads = 1;
     DevBuf out_samples, out_grads, out_bits, out_tmp, stage_samples, stage_grads;
 };
+
+// Transfers are ordered on the context's (non-blocking) stream, after every kernel queued there,
+// and waited for before the host buffer is released.
+static hipError_t h2d(mcmc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e;
+}
+static hipError_t d2h(mcmc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e;
+}
+static hipError_t dzero(mcmc_ctx* ctx, void* dst, size_t bytes) {
+    return hipMemsetAsync(dst, 0, bytes, ctx->stream);
+}
 
 static int set_device(mcmc_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->device));
@@ -299,7 +318,7 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
                     if (!(desc->Y[i] == 0.0 || desc->Y[i] == 1.0))
                         return bail(fail(MCMC_E_INVALID_ARG, "logistic responses must be 0 or 1 (Bernoulli)"));
             // X_pad [n_pad][d_pad] row-major, zero rows/columns past (n, d) (glm.hip geometry)
-            const int64_t d_pad = d <= 128 ? (d + 15) / 16 * 16 : (d + 127) / 128 * 128;
+            const int64_t d_pad = mcmc_glm_d_pad((int)d);
             const int64_t n_pad = (desc->n + 15) / 16 * 16;
             std::vector<double> Xp((size_t)n_pad * d_pad, 0.0), Yp((size_t)n_pad, 0.0);
             for (int64_t i = 0; i < desc->n; ++i) {
@@ -308,8 +327,8 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
             }
             if (int r = dmalloc(&m->d_X, Xp.size())) return bail(r);
             if (int r = dmalloc(&m->d_Y, Yp.size())) return bail(r);
-            if (hipMemcpy(m->d_X, Xp.data(), Xp.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(m->d_Y, Yp.data(), Yp.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+            if (h2d(ctx, m->d_X, Xp.data(), Xp.size() * 8) != hipSuccess ||
+                h2d(ctx, m->d_Y, Yp.data(), Yp.size() * 8) != hipSuccess)
                 return bail(fail(MCMC_E_HIP, "model data upload failed"));
             a.n = desc->n;
             a.n_pad = n_pad;
@@ -324,8 +343,8 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
     if (int r = dmalloc(&m->d_init, (size_t)d)) return bail(r);
     if (int r = dmalloc(&m->d_scale, (size_t)d)) return bail(r);
     a.init = m->d_init;
-    hipError_t e = hipMemcpy(m->d_init, m->init.data(), (size_t)d * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(m->d_scale, m->scale.data(), (size_t)d * 8, hipMemcpyHostToDevice);
+    hipError_t e = h2d(ctx, m->d_init, m->init.data(), (size_t)d * 8);
+    if (e == hipSuccess) e = h2d(ctx, m->d_scale, m->scale.data(), (size_t)d * 8);
     if (e != hipSuccess) return bail(fail(MCMC_E_HIP, std::string("model upload: ") + hipGetErrorString(e)));
     // likmodel.jl:54  @assert isfinite(f(i)) "Initial values out of model support, try other values"
     double lp = 0;
@@ -336,14 +355,21 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
     return MCMC_OK;
 }
 
-extern "C" int mcmc_model_destroy(mcmc_model* m) {
-    if (!m) return MCMC_OK;
+static void model_free(mcmc_model* m) {
     (void)hipSetDevice(m->ctx->device);
     dfree(m->d_init);
     dfree(m->d_scale);
     dfree(m->d_X);
     dfree(m->d_Y);
     delete m;
+}
+
+// A model outlives its chains: destroying it while chains still use it (garbage-collected hosts
+// finalize in any order) only marks it; the last mcmc_chains_destroy frees it.
+extern "C" int mcmc_model_destroy(mcmc_model* m) {
+    if (!m) return MCMC_OK;
+    m->released = true;
+    if (m->chains_alive == 0) model_free(m);
     return MCMC_OK;
 }
 
@@ -453,10 +479,10 @@ static int init_state(mcmc_chains* c) {
     HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int32_t), st));
     if (c->d_init_x) {
         HIP_TRY(cols_to_state(c->layout, c->st.x, c->ld, c->d_init_x, c->C, d, c->C, st));
-    } else if (c->layout == LAYOUT_LPC) {
-        HIP_TRY(mcmc_broadcast_cols(c->st.x, c->ld, m->d_init, d, c->C, st));
-    } else {
+    } else if (c->layout == LAYOUT_WPC) {       // chain-major [C][ld]
         HIP_TRY(mcmc_broadcast_rows(c->st.x, c->ld, m->d_init, d, c->C, st));
+    } else {                                    // coordinate-major [d][ld] (LPC, GLM)
+        HIP_TRY(mcmc_broadcast_cols(c->st.x, c->ld, m->d_init, d, c->C, st));
     }
     KernelArgs a = base_args(m, c->C, c->ld);
     HIP_TRY(launch_eval(c->layout, a, c->st.x, c->st.lp, c->st.g, 1, st));
@@ -503,6 +529,7 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
         return fail(MCMC_E_UNSUPPORTED, "separable targets support d <= 2048");
     auto* c = new mcmc_chains();
     c->model = m;
+    m->chains_alive += 1;
     c->C = nchains;
     c->layout = layout_for(m);
     c->ld = ld_for(c->layout, nchains, d);
@@ -553,12 +580,12 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (sa.kind == SK_RWM)
         for (auto& v : se) v = v * sa.scale;
     if (int r = dmalloc(&c->d_scale_eff, (size_t)round_up(d, 256))) return bail(r);
-    if (hipMemset(c->d_scale_eff, 0, (size_t)round_up(d, 256) * 8) != hipSuccess ||
-        hipMemcpy(c->d_scale_eff, se.data(), (size_t)d * 8, hipMemcpyHostToDevice) != hipSuccess)
+    if (dzero(ctx, c->d_scale_eff, (size_t)round_up(d, 256) * 8) != hipSuccess ||
+        h2d(ctx, c->d_scale_eff, se.data(), (size_t)d * 8) != hipSuccess)
         return bail(fail(MCMC_E_HIP, "scale upload failed"));
     if (init_x) {
         if (int r = dmalloc(&c->d_init_x, (size_t)d * nchains)) return bail(r);
-        if (hipMemcpy(c->d_init_x, init_x, (size_t)d * nchains * 8, hipMemcpyHostToDevice) != hipSuccess)
+        if (h2d(ctx, c->d_init_x, init_x, (size_t)d * nchains * 8) != hipSuccess)
             return bail(fail(MCMC_E_HIP, "init_x upload failed"));
     }
     if (int r = init_state(c)) return bail(r);
@@ -579,7 +606,9 @@ extern "C" int mcmc_chains_destroy(mcmc_chains* c) {
     dfree(c->out_tmp.p);
     dfree(c->stage_samples.p);
     dfree(c->stage_grads.p);
+    mcmc_model* m = c->model;
     delete c;
+    if (--m->chains_alive == 0 && m->released) model_free(m);
     return MCMC_OK;
 }
 
@@ -681,6 +710,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     s.len = r->len;
     s.tuner_burnin = r->burnin;
     s.scale = c->d_scale_eff;
+
     s.samples = k_samples;
     s.grads = k_grads;
     s.acc_bits = d_bits;
@@ -713,9 +743,9 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
         out->runtime_s = std::chrono::duration<double>(t1 - t0).count();
         out->kernel_ms = ms;
         if (!on_dev) {
-            if (want_samples) HIP_TRY(hipMemcpy(out->samples, d_samples, nsamp * 8, hipMemcpyDeviceToHost));
-            if (want_grads) HIP_TRY(hipMemcpy(out->gradients, d_grads, nsamp * 8, hipMemcpyDeviceToHost));
-            if (want_bits) HIP_TRY(hipMemcpy(out->accept_bits, d_bits, (size_t)nkept * nw * 8, hipMemcpyDeviceToHost));
+            if (want_samples) HIP_TRY(d2h(ctx, out->samples, d_samples, nsamp * 8));
+            if (want_grads) HIP_TRY(d2h(ctx, out->gradients, d_grads, nsamp * 8));
+            if (want_bits) HIP_TRY(d2h(ctx, out->accept_bits, d_bits, (size_t)nkept * nw * 8));
         }
         if (out->final_x) {
             if (on_dev) {
@@ -745,11 +775,11 @@ extern "C" int mcmc_debug_detmath(mcmc_ctx* ctx, int op, int64_t n, const double
         if ((rc = dmalloc(&dx, (size_t)n))) break;
         if ((rc = dmalloc(&dy, (size_t)n))) break;
         if ((rc = dmalloc(&dout, nout))) break;
-        hipError_t e = hipMemcpy(dx, x, (size_t)n * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess && y) e = hipMemcpy(dy, y, (size_t)n * 8, hipMemcpyHostToDevice);
+        hipError_t e = h2d(ctx, dx, x, (size_t)n * 8);
+        if (e == hipSuccess && y) e = h2d(ctx, dy, y, (size_t)n * 8);
         if (e == hipSuccess) e = mcmc_detmath(op, n, dx, dy, dout, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e == hipSuccess) e = hipMemcpy(out, dout, nout * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = d2h(ctx, out, dout, nout * 8);
         if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("detmath probe: ") + hipGetErrorString(e));
     } while (0);
     dfree(dx);
@@ -767,11 +797,11 @@ extern "C" int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr, 
         if ((rc = dmalloc(&dc, 4 * (size_t)n))) break;
         if ((rc = dmalloc(&dk, 2 * (size_t)n))) break;
         if ((rc = dmalloc(&dout, 4 * (size_t)n))) break;
-        hipError_t e = hipMemcpy(dc, ctr, 16 * (size_t)n, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(dk, key, 8 * (size_t)n, hipMemcpyHostToDevice);
+        hipError_t e = h2d(ctx, dc, ctr, 16 * (size_t)n);
+        if (e == hipSuccess) e = h2d(ctx, dk, key, 8 * (size_t)n);
         if (e == hipSuccess) e = mcmc_philox(n, dc, dk, dout, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e == hipSuccess) e = hipMemcpy(out, dout, 16 * (size_t)n, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = d2h(ctx, out, dout, 16 * (size_t)n);
         if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("philox probe: ") + hipGetErrorString(e));
     } while (0);
     dfree(dc);
@@ -791,12 +821,12 @@ extern "C" int mcmc_debug_mfma_f64(mcmc_ctx* ctx, int nk, const double* A, const
         if ((rc = dmalloc(&dB, 64 * (size_t)nk))) break;
         if ((rc = dmalloc(&dC, 256))) break;
         if ((rc = dmalloc(&dD, 256))) break;
-        hipError_t e = hipMemcpy(dA, A, 512 * (size_t)nk, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(dB, B, 512 * (size_t)nk, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(dC, C, 2048, hipMemcpyHostToDevice);
+        hipError_t e = h2d(ctx, dA, A, 512 * (size_t)nk);
+        if (e == hipSuccess) e = h2d(ctx, dB, B, 512 * (size_t)nk);
+        if (e == hipSuccess) e = h2d(ctx, dC, C, 2048);
         if (e == hipSuccess) e = mcmc_mfma_probe(dA, dB, dC, dD, nk, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e == hipSuccess) e = hipMemcpy(D, dD, 2048, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = d2h(ctx, D, dD, 2048);
         if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("mfma probe: ") + hipGetErrorString(e));
     } while (0);
     dfree(dA); dfree(dB); dfree(dC); dfree(dD);

@@ -684,6 +684,8 @@ mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
 
 int mcmc_glm_max_d() { return 512; }
 
+int mcmc_glm_d_pad(int d) { return mcmc_glm_shape(d, 1).d_pad; }
+
 template <int NM, int NW>
 static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
     using namespace mcmc;

@@ -127,7 +127,7 @@ def test_sampler_parity(gpu, sname, mkind, d):
     oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=C, seed=12345 + d, order=order_for(d))
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
-    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert np.array_equal(chain.final_x, oc.x, equal_nan=True) and np.array_equal(chain.final_lp, oc.lp, equal_nan=True)
 
 
 @pytest.mark.parametrize("d", [5, 70])
@@ -254,7 +254,7 @@ def test_glm_sampler_parity(gpu, sname, kind, d):
     oc = orc.OracleChains(m, GLM_SAMPLERS[sname](), nchains=C, seed=99 + d)
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
-    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert np.array_equal(chain.final_x, oc.x, equal_nan=True) and np.array_equal(chain.final_lp, oc.lp, equal_nan=True)
 
 
 @pytest.mark.parametrize("kind", ["logistic", "linear"])
@@ -294,3 +294,35 @@ def test_logistic_out_of_support_rejects(gpu):
     oc = orc.OracleChains(m, mc.RWM(50.0), nchains=20, seed=1)
     s, g, acc = oc.run(r)
     assert_parity(ch, s, g, acc, "rwm")
+
+
+@pytest.mark.parametrize("sname", ["rwm", "hmc"])
+def test_glm_nonzero_init_few_coords_many_chains(gpu, sname):
+    """d << C with a non-zero start: the coordinate-major state must be broadcast per coordinate row."""
+    d = 5
+    rng = np.random.default_rng(11)
+    X = np.hstack([np.ones((60, 1)), rng.normal(size=(60, d - 1))])
+    Y = X @ (rng.normal(size=d) * 0.3) + rng.normal(size=60)
+    m = mc.model(mc.LinearRegression(X, Y), vars=0.1 * np.arange(1, d + 1), gradient=True)
+    r = mc.SerialMC(steps=9, burnin=1, thinning=2)
+    ch = mc.run((m * GLM_SAMPLERS[sname]() * r).batch(200, seed=3))
+    oc = orc.OracleChains(m, GLM_SAMPLERS[sname](), nchains=200, seed=3)
+    s, g, acc = oc.run(r)
+    assert_parity(ch, s, g, acc, sname)
+
+
+def test_model_released_before_its_chains(gpu):
+    """A host that finalizes the model before its chains (any GC order) must not free it under them."""
+    from mcmchip import _lib
+    m = _glm_model("logistic", 6)
+    r = mc.SerialMC(steps=5)
+    t = (m * mc.HMC(2, 0.05) * r).batch(32, seed=2)
+    t.handle()
+    for h in m._dev.values():
+        _lib.check(_lib.load().mcmc_model_destroy(h))
+    m._dev.clear()
+    ch = mc.run(t)                          # the chains still own a live model
+    oc = orc.OracleChains(m, mc.HMC(2, 0.05), nchains=32, seed=2)
+    s, g, acc = oc.run(r)
+    assert_parity(ch, s, g, acc, "hmc")
+    del t, ch                               # last chains gone: the model is freed now
