@@ -161,6 +161,10 @@ int mcmc_chains_destroy(mcmc_chains* chains);
 int mcmc_chains_reset(mcmc_chains* chains);
 /* steps consumed so far (the sampler's own loop counter i). */
 int mcmc_chains_steps_done(mcmc_chains* chains, int64_t* steps);
+/* log-target evaluations (with gradient for MALA/HMC/HMCDA) summed over all chains since
+ * create/reset: steps x C for RWM/MALA, the leapfrog count for HMC/HMCDA (HMC.jl:219-228),
+ * whose trajectory length varies per chain under HMCDA / EmpMCTuner. */
+int mcmc_chains_evals(mcmc_chains* chains, int64_t* evals);
 /* steps fused per kernel launch (0 = whole run in one launch, the default). */
 int mcmc_chains_set_steps_per_launch(mcmc_chains* chains, int64_t steps_per_launch);
 /* store gradients of kept samples for gradient samplers (default 1, SerialMC.jl:51-53) */

@@ -67,6 +67,7 @@ struct StepArgs {
     uint64_t* acc_bits;         // [nkept][nw]
     int64_t nw;                 // words per kept step = ceil(C/64)
     int32_t* err;               // device error word
+    unsigned long long* n_evals;  // running count of log-target evaluations over all chains (NULL: off)
 };
 
 __host__ __device__ inline bool kept_index(int64_t i_loc, int64_t burnin, int64_t thinning, int64_t len,

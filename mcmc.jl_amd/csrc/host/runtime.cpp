@@ -85,6 +85,7 @@ struct mcmc_chains {
     ChainState st{};
     double* d_scale_eff = nullptr;   // model.scale .* sampler.scale (RWM.jl:52)
     double* d_init_x = nullptr;      // optional per-chain start, [d][C]
+    unsigned long long* d_evals = nullptr;   // log-target evaluations since create/reset (all chains)
     int64_t steps_done = 0;
     int64_t spl = 0;                 // steps per launch (0: whole run)
     int store_grads = 1;
@@ -477,6 +478,7 @@ static int init_state(mcmc_chains* c) {
     const SamplerArgs& sa = c->sa;
     hipStream_t st = ctx->stream;
     HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), st));
     if (c->d_init_x) {
         HIP_TRY(cols_to_state(c->layout, c->st.x, c->ld, c->d_init_x, c->C, d, c->C, st));
     } else if (c->layout == LAYOUT_WPC) {       // chain-major [C][ld]
@@ -580,6 +582,7 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (sa.kind == SK_RWM)
         for (auto& v : se) v = v * sa.scale;
     if (int r = dmalloc(&c->d_scale_eff, (size_t)round_up(d, 256))) return bail(r);
+    if (int r = dmalloc(&c->d_evals, 1)) return bail(r);
     if (dzero(ctx, c->d_scale_eff, (size_t)round_up(d, 256) * 8) != hipSuccess ||
         h2d(ctx, c->d_scale_eff, se.data(), (size_t)d * 8) != hipSuccess)
         return bail(fail(MCMC_E_HIP, "scale upload failed"));
@@ -600,6 +603,7 @@ extern "C" int mcmc_chains_destroy(mcmc_chains* c) {
     free_state(c);
     dfree(c->d_scale_eff);
     dfree(c->d_init_x);
+    dfree(c->d_evals);
     dfree(c->out_samples.p);
     dfree(c->out_grads.p);
     dfree(c->out_bits.p);
@@ -616,6 +620,16 @@ extern "C" int mcmc_chains_reset(mcmc_chains* c) {
     if (!c) return fail(MCMC_E_INVALID_ARG, "chains is NULL");
     if (int r = set_device(c->model->ctx)) return r;
     return init_state(c);
+}
+
+extern "C" int mcmc_chains_evals(mcmc_chains* c, int64_t* evals) {
+    if (!c || !evals) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    mcmc_ctx* ctx = c->model->ctx;
+    if (int r = set_device(ctx)) return r;
+    unsigned long long v = 0;
+    HIP_TRY(d2h(ctx, &v, c->d_evals, sizeof v));
+    *evals = (int64_t)v;
+    return MCMC_OK;
 }
 
 extern "C" int mcmc_chains_steps_done(mcmc_chains* c, int64_t* steps) {
@@ -715,6 +729,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     s.grads = k_grads;
     s.acc_bits = d_bits;
     s.nw = nw;
+    s.n_evals = c->d_evals;
 
     const int64_t spl = c->spl > 0 ? c->spl : r->len;
     HIP_TRY(hipStreamSynchronize(st));

@@ -338,6 +338,14 @@ __device__ __forceinline__ void glm_store_kept4(const GlmArgs& a, const GlmPos& 
     if (base == nullptr) return;
     glm_store4<NM>(a, p, base + (size_t)kk * (size_t)a.s.d * (size_t)a.s.C, a.s.C, v);
 }
+// add the tile's evaluation counts to the launch-wide counter (one atomic per wave)
+__device__ __forceinline__ void glm_count_evals(const GlmArgs& a, const GlmPos& p, int64_t n) {
+    if (a.s.n_evals == nullptr) return;
+    unsigned long long v = (p.live && p.q == 0 && p.slice == 0) ? (unsigned long long)n : 0ull;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (p.lane == 0) atomicAdd(a.s.n_evals, v);
+}
 __device__ __forceinline__ void glm_store_bit(const GlmArgs& a, const GlmPos& p, int64_t kk, bool acc) {
     if (p.live && acc && p.q == 0 && p.slice == 0 && a.s.acc_bits != nullptr)
         atomicOr((unsigned long long*)&a.s.acc_bits[(size_t)kk * (size_t)a.s.nw + (size_t)(p.c >> 6)],
@@ -431,6 +439,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_rwm(GlmArgs a) {
         }
     }
     if (p.live && p.q == 0 && p.slice == 0) a.st.lp[p.c] = lp;
+    glm_count_evals(a, p, s.nsteps);
 }
 
 template <int NM, int NW>
@@ -516,6 +525,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_mala(GlmArgs a) {
             a.st.t_prop[p.c] = n_prop;
         }
     }
+    glm_count_evals(a, p, s.nsteps);
 }
 
 template <int NM, int NW, bool DA>
@@ -538,6 +548,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
     int32_t n_acc = tuned ? a.st.t_acc[cc] : 0;
     int32_t n_prop = tuned ? a.st.t_prop[cc] : 0;
     const double mu = DA ? det_log(10.0) : 0.0;
+    int64_t n_evals = 0;
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         if (tuned) n_prop += 1;
@@ -558,6 +569,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
         } else {
             nl = nl_fixed;
         }
+        n_evals += nl;
         const int64_t nl_wg = (DA || tuned) ? glm_max(L, nl, p.live) : nl;
         double lpl = lp;
         for (int64_t l = 0; l < nl_wg; ++l) {
@@ -640,6 +652,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
             a.st.t_prop[p.c] = n_prop;
         }
     }
+    glm_count_evals(a, p, n_evals);
 }
 
 static GlmArgs glm_args(const KernelArgs& k, const GlmShape& g) {

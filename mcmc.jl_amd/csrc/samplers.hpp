@@ -76,6 +76,14 @@ struct LaneChain {
         for (int k = 0; k < NC; ++k)
             if (valid(k)) p[(size_t)k * (size_t)s.C] = v[k];
     }
+    // add this chain's evaluation count to the launch-wide counter (one atomic per wave)
+    __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
+        if (s.n_evals == nullptr) return;
+        unsigned long long v = live ? (unsigned long long)n : 0ull;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(s.n_evals, v);
+    }
     __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
         const uint64_t mask = __ballot(acc && live);
         if ((threadIdx.x & 63) == 0 && s.acc_bits != nullptr) {
@@ -156,6 +164,9 @@ struct WaveChain {
             if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
                                                                                v[4 * g + 3]);
         }
+    }
+    __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
+        if (s.n_evals != nullptr && live && lane == 0) atomicAdd(s.n_evals, (unsigned long long)n);
     }
     __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
         if (live && lane == 0 && acc && s.acc_bits != nullptr)
@@ -246,6 +257,7 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     }
     p.store(a.st.x, s.ld, x);
     p.store_t(a.st.lp, lp);
+    p.count_evals(s, s.nsteps);
 }
 
 // ------------------------------------------------------------------ MALA
@@ -319,6 +331,7 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
     }
     p.store(a.st.x, s.ld, x);
     p.store_t(a.st.lp, lp);
+    p.count_evals(s, s.nsteps);
     if (sa.tuner) {
         p.store_t(a.st.t_step, h);
         p.store_t(a.st.t_acc, n_acc);
@@ -372,6 +385,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
     int32_t n_prop = tuned ? p.load_t(a.st.t_prop) : 0;
     const double mu = DA ? det_log(10.0) : 0.0;                 // log(10*leapStep0), leapStep0 = 1
 
+    int64_t n_evals = 0;
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         if (tuned) n_prop += 1;
@@ -387,6 +401,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
         } else {
             nl = nl_fixed;
         }
+        n_evals += nl;
         const double lpl = trajectory(p, model, eps, nl, x, m);
         const double H = -lpl + half_dot(p, m);
         const u32x4 w = rs.block(chain, (uint32_t)i, 0u, TAG_ACCEPT);
@@ -437,6 +452,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             n_prop = 0;
         }
     }
+    p.count_evals(s, n_evals);
     p.store(a.st.x, s.ld, x0);
     p.store_t(a.st.lp, lp);
     if (DA || tuned) p.store_t(a.st.t_step, eps);

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_ctx_create", "mcmc_ctx_destroy", "mcmc_ctx_synchronize",
     "mcmc_model_create", "mcmc_model_destroy", "mcmc_model_eval",
     "mcmc_sampler_validate", "mcmc_runner_validate",
-    "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done",
+    "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done", "mcmc_chains_evals",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients",
     "mcmc_run_serialmc", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
 )
@@ -119,6 +119,7 @@ def load() -> ct.CDLL:
         "mcmc_chains_destroy": (ct.c_int, [P]),
         "mcmc_chains_reset": (ct.c_int, [P]),
         "mcmc_chains_steps_done": (ct.c_int, [P, ct.POINTER(i64)]),
+        "mcmc_chains_evals": (ct.c_int, [P, ct.POINTER(i64)]),
         "mcmc_chains_set_steps_per_launch": (ct.c_int, [P, i64]),
         "mcmc_chains_set_store_gradients": (ct.c_int, [P, i32]),
         "mcmc_run_serialmc": (ct.c_int, [P, ct.POINTER(RunnerCfg), ct.POINTER(Outputs)]),

@@ -435,6 +435,15 @@ class MCMCTask:
         check(_lib.load().mcmc_chains_steps_done(self._h, ct.byref(v)))
         return v.value
 
+    @property
+    def evals(self) -> int:
+        """Log-target evaluations over all chains since the chains were created/reset."""
+        if self._h is None:
+            return 0
+        v = ct.c_int64(0)
+        check(_lib.load().mcmc_chains_evals(self._h, ct.byref(v)))
+        return v.value
+
     def reset(self) -> None:
         if self._h is not None:
             check(_lib.load().mcmc_chains_reset(self._h))

@@ -69,6 +69,7 @@ typedef struct {
     int32_t* t_leaps;
     int32_t* t_acc;
     int32_t* t_prop;
+    int64_t* n_evals;   /* log-target evaluations per chain (steps for RWM/MALA, leapfrogs for HMC) */
 } orc_state;
 
 static const double ORC_LOG2PI = 0x1.d67f1c864beb5p+0;
@@ -359,6 +360,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
     double h_bar = s->kind == ORC_HMCDA ? st->t_h[c] : 0.0;
     int32_t n_acc = tuned ? st->t_acc[c] : 0;
     int32_t n_prop = tuned ? st->t_prop[c] : 0;
+    int64_t n_evals = 0;
     const double mu = orc_log(10.0);          /* HMCDA.jl:92: mu = log(10*leapStep) with leapStep = 1 */
     const int64_t max_leaps = s->max_leaps > 0 ? s->max_leaps : ((int64_t)1 << 20);
 
@@ -421,6 +423,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
             } else {
                 nl = nl_fixed;
             }
+            n_evals += nl;
             double lpl = orc_trajectory(m, eps, nl, xp, mom, gp, lp, tmp, order);
             const double H = -lpl + 0.5 * orc_dot(mom, m, order);
             const double u = orc_accept_uniform(seed, chain, (uint32_t)i);
@@ -473,6 +476,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
     }
     for (int j = 0; j < d; ++j) st->x[(size_t)j * C + c] = x[j];
     st->lp[c] = lp;
+    if (st->n_evals) st->n_evals[c] += (s->kind == ORC_RWM || s->kind == ORC_MALA) ? len : n_evals;
     if (tuned || s->kind == ORC_HMCDA) st->t_step[c] = (s->kind == ORC_MALA) ? h : eps;
     if (s->kind == ORC_HMCDA) {
         st->t_bar[c] = eps_bar;
@@ -510,6 +514,7 @@ int64_t orc_init(const orc_model* m, const orc_sampler* s, int64_t C, orc_state*
         if (s->kind == ORC_HMC && tuned) { st->t_step[c] = s->leap_step; st->t_leaps[c] = (int32_t)s->n_leaps; }
         if (s->kind == ORC_HMCDA) { st->t_step[c] = 1.0; st->t_bar[c] = 1.0; st->t_h[c] = 0.0; }
         if (tuned) { st->t_acc[c] = 0; st->t_prop[c] = 0; }
+        if (st->n_evals) st->n_evals[c] = 0;
     }
     free(buf);
     return bad;

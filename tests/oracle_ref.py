@@ -37,7 +37,7 @@ class OSampler(ct.Structure):
 class OState(ct.Structure):
     _fields_ = [("x", D), ("lp", D), ("t_step", D), ("t_bar", D), ("t_h", D),
                 ("t_leaps", ct.POINTER(ct.c_int32)), ("t_acc", ct.POINTER(ct.c_int32)),
-                ("t_prop", ct.POINTER(ct.c_int32))]
+                ("t_prop", ct.POINTER(ct.c_int32)), ("n_evals", ct.POINTER(ct.c_int64))]
 
 
 _lib = None
@@ -135,8 +135,10 @@ class OracleChains:
         self.t_leaps = np.zeros(C, dtype=np.int32)
         self.t_acc = np.zeros(C, dtype=np.int32)
         self.t_prop = np.zeros(C, dtype=np.int32)
+        self.n_evals = np.zeros(C, dtype=np.int64)
         self.st = OState(_d(self.x), _d(self.lp), _d(self.t_step), _d(self.t_bar), _d(self.t_h),
-                         _i(self.t_leaps), _i(self.t_acc), _i(self.t_prop))
+                         _i(self.t_leaps), _i(self.t_acc), _i(self.t_prop),
+                         self.n_evals.ctypes.data_as(ct.POINTER(ct.c_int64)))
         bad = lib().orc_init(ct.byref(self.om.s), ct.byref(self.os), C, ct.byref(self.st), self.order)
         if bad:
             raise AssertionError("Initial values out of model support, try other values")

@@ -128,6 +128,7 @@ def test_sampler_parity(gpu, sname, mkind, d):
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
     assert np.array_equal(chain.final_x, oc.x, equal_nan=True) and np.array_equal(chain.final_lp, oc.lp, equal_nan=True)
+    assert chain.task.evals == int(oc.n_evals.sum())        # leapfrog / evaluation bookkeeping
 
 
 @pytest.mark.parametrize("d", [5, 70])
@@ -255,6 +256,7 @@ def test_glm_sampler_parity(gpu, sname, kind, d):
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
     assert np.array_equal(chain.final_x, oc.x, equal_nan=True) and np.array_equal(chain.final_lp, oc.lp, equal_nan=True)
+    assert chain.task.evals == int(oc.n_evals.sum())        # leapfrog / evaluation bookkeeping
 
 
 @pytest.mark.parametrize("kind", ["logistic", "linear"])
