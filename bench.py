@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the many-chain MCMC inner loop (BASELINE.json metric).
 
-Workload (BASELINE.json "metric" config): d = 32 iso-Normal target -dot(v,v),
+Default workload (BASELINE.json "metric"): d = 32 iso-Normal target -dot(v,v),
 RWM(0.1), init ones(32), SerialMC(steps=1000, burnin=100, thinning=10), 2^20
-chains per GPU, seed 1, fp64.  A "step" is one MCMC step of every chain
-(one pass of the hot path over the chain batch).  The timed region runs
-`--steps` steps through run_serialmc with kept samples, gradients and accept
-bits written to HBM (device-resident outputs); chain state is resident in HBM
-before the clock starts.
+chains per GPU, seed 1, fp64.  A "step" is one MCMC step of every chain (one
+pass of the hot path over the chain batch).  The timed region is one
+run_serialmc call of `--steps` steps with kept samples, gradients and accept
+bits written to device-resident outputs; chain state and model data are in
+HBM before the clock starts.
 
-  python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, weak scaling:
-                                                      every rank runs 2^20 chains)
+Other BASELINE.json configs (--config): readme (config 1), d3 (config 2),
+logistic128 (config 3), hmc1024 (config 4, per-GPU shard), linear512
+(config 5, per-GPU shard).
+
+  python bench.py [--config metric] [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU; weak scaling:
+                                                      every rank runs the per-GPU chain count)
 Prints one JSON line (rank 0).
 """
 from __future__ import annotations
@@ -29,27 +33,34 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mcmc.jl_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+F64_MFMA_PEAK_TFS = 78.6       # MI355X spec, dense fp64 matrix (not in the guide; measured in DESIGN.md §7)
 
-# BASELINE.json configs (per-GPU chain counts for the sharded ones)
+# BASELINE.json configs.  chains are per GPU; steps/warmup are the defaults when not given.
 CONFIGS = {
-    "metric": dict(d=32, chains=1 << 20, sampler="rwm", thinning=10,
+    "metric": dict(model="iso", d=32, chains=1 << 20, sampler="rwm", steps=1000, warmup=100, thinning=10,
                    desc="d=32 iso-Normal, RWM(0.1), 2^20 chains/GPU (BASELINE metric)"),
-    "readme": dict(d=3, chains=1, sampler="rwm", thinning=1,
+    "readme": dict(model="iso", d=3, chains=1, sampler="rwm", steps=1000, warmup=100, thinning=1,
                    desc="config 1: d=3 iso-Normal, RWM(0.1), SerialMC(1000,100), 1 chain"),
-    "d3": dict(d=3, chains=1 << 20, sampler="rwm", thinning=10,
+    "d3": dict(model="iso", d=3, chains=1 << 20, sampler="rwm", steps=1000, warmup=100, thinning=10,
                desc="config 2: d=3 iso-Normal, RWM(0.1), 1,048,576 chains"),
-    "hmc1024": dict(d=1024, chains=524288 // 8, sampler="hmc", thinning=100,
-                    desc="config 4: d=1024 iso-Normal, HMC(10, 0.1), 524,288 chains over 8 GPUs (65,536/GPU)"),
+    "logistic128": dict(model="logistic", d=128, n=1000, chains=262144, sampler="mala", steps=200, warmup=10,
+                        thinning=10, desc="config 3: logistic regression n=1000 d=128, MALA(0.001), "
+                                          "262,144 chains"),
+    "hmc1024": dict(model="iso", d=1024, chains=524288 // 8, sampler="hmc", steps=1000, warmup=100,
+                    thinning=100, desc="config 4: d=1024 iso-Normal, HMC(10, 0.1), 524,288 chains over 8 GPUs "
+                                       "(65,536/GPU)"),
+    "linear512": dict(model="linear", d=512, n=4096, chains=65536 // 8, sampler="hmcda", steps=20, warmup=2,
+                      thinning=1, desc="config 5: linear regression n=4096 d=512, HMCDA(), 65,536 chains over 8 "
+                                       "GPUs (8,192/GPU); 20 steps: each step is ~len/eps leapfrogs"),
 }
 
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--config", default="metric", choices=list(CONFIGS),
-                   help="BASELINE.json workload (metric = 2^20 chains x d=32 RWM)")
+    p.add_argument("--config", default="metric", choices=list(CONFIGS))
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1000)
-    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--d", type=int, default=None)
     p.add_argument("--chains", type=int, default=None, help="chains per GPU")
     p.add_argument("--sampler", default=None, choices=["rwm", "mala", "hmc", "hmcda"])
@@ -62,28 +73,66 @@ def parse():
     return p.parse_args()
 
 
-def algorithmic_bytes(d, C, steps, burnin, thinning, spl, grad_sampler):
-    """state round trip 16d + 16 B per chain per launch-step of state traffic,
-    8d B per kept chain-step (+8d for gradients), 1 bit per kept chain-step."""
-    nkept = len(range(burnin + 1, steps + 1, thinning))
-    launches = 1 if spl == 0 else -(-steps // spl)
-    state = launches * C * (16 * d + 16)
-    kept = nkept * C * (8 * d * (2 if grad_sampler else 1)) + nkept * ((C + 63) // 64) * 8
-    return state + kept, launches
+def regression_data(kind, n, d, key=0x5EED):
+    """X = [1 | N(0,1)], beta0 ~ N(0,1); Y Bernoulli(logistic(X beta0)) or
+    X beta0 + N(0,1).  Drawn from numpy's Philox4x32-10 on its own key (not the chains' stream)."""
+    g = np.random.Generator(np.random.Philox(key=key))
+    X = np.hstack([np.ones((n, 1)), g.standard_normal((n, d - 1))])
+    beta0 = g.standard_normal(d)
+    eta = X @ beta0
+    if kind == "logistic":
+        Y = (g.random(n) < 1.0 / (1.0 + np.exp(-eta))).astype(np.float64)
+    else:
+        Y = eta + g.standard_normal(n)
+    return X, Y
 
 
-def cpu_baseline(args, model, sampler, seconds):
+def build_model(mc, cfg, d):
+    if cfg["model"] == "iso":
+        return mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
+    X, Y = regression_data(cfg["model"], cfg["n"], d)
+    if cfg["model"] == "logistic":
+        return mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(d), gradient=True)
+    return mc.model(mc.LinearRegression(X, Y), vars=np.zeros(d), gradient=True)
+
+
+def build_sampler(mc, cfg, name):
+    if cfg["model"] == "logistic" and name == "mala":
+        return mc.MALA(0.001)                        # test/test_syntax.jl:28
+    return {"rwm": lambda: mc.RWM(0.1), "mala": lambda: mc.MALA(0.1), "hmc": lambda: mc.HMC(10, 0.1),
+            "hmcda": lambda: mc.HMCDA()}[name]()
+
+
+def hbm_bytes_per_unit(d, sampler):
+    """SURVEY.md §8(d) algorithmic bytes per chain-step (state round trip + 1 accept bit) and per kept
+    chain-step (sample, + gradient for gradient samplers)."""
+    per_step = (32 * d if sampler == "mala" else 16 * d) + 16 + 1 / 8
+    per_kept = 8 * d * (1 if sampler == "rwm" else 2)
+    return per_step, per_kept
+
+
+def kernel_name(cfg, d, sampler):
+    if cfg["model"] != "iso":
+        nm = 1
+        while d <= 64 and 16 * nm < d:
+            nm *= 2
+        nw = 1 if d <= 64 else next(w for w in (2, 4, 8) if 64 * w >= d)
+        nm = nm if d <= 64 else 4
+        return f"glm_{'hmc' if sampler.startswith('hmc') else sampler}<{nm},{nw}{',DA' if sampler == 'hmcda' else ''}>"
+    return f"{'lpc' if d <= 32 else 'wpc'}_{sampler}"
+
+
+def cpu_baseline(model, sampler, seconds, C=4096):
     """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref as orc
     import mcmchip as mc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
-    C = 4096
-    steps = 50
+    steps = 4
     t0 = time.perf_counter()
     oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
-    oc.run(mc.SerialMC(steps=steps, burnin=5, thinning=10), nthreads=threads)
+    oc.run(mc.SerialMC(steps=steps, burnin=1, thinning=1), nthreads=threads)
     dt = time.perf_counter() - t0
     rate = C * steps / dt
     steps2 = max(steps, int(rate * seconds / C))
@@ -93,7 +142,7 @@ def cpu_baseline(args, model, sampler, seconds):
     dt = time.perf_counter() - t0
     return {"value": C * steps2 / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
             "sample": f"{C} chains x {steps2} steps of the same workload on the host ({dt:.1f} s), "
-                      f"oracle/oracle.c OpenMP over chains; the GPU run's chain count scales it linearly"}
+                      f"oracle/oracle.c OpenMP over chains; chains are independent, so the rate is per chain-step"}
 
 
 def main():
@@ -111,14 +160,13 @@ def main():
     from mcmchip import _lib
 
     cfg0 = CONFIGS[args.config]
-    for k in ("d", "chains", "sampler", "thinning"):
+    for k in ("d", "chains", "sampler", "thinning", "steps", "warmup"):
         if getattr(args, k) is None:
             setattr(args, k, cfg0[k])
     d = args.d
     C = max(1, args.chains // world) if args.strong else args.chains
-    model = mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
-    sampler = {"rwm": lambda: mc.RWM(0.1), "mala": lambda: mc.MALA(0.1), "hmc": lambda: mc.HMC(10, 0.1),
-               "hmcda": lambda: mc.HMCDA()}[args.sampler]()
+    model = build_model(mc, cfg0, d)
+    sampler = build_sampler(mc, cfg0, args.sampler)
     K, W = args.steps, args.warmup
     burnin = K // 10
     runner = mc.SerialMC(steps=K, burnin=burnin, thinning=args.thinning)
@@ -146,6 +194,7 @@ def main():
         cfg = wr.cfg()
         _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(wout)))
     torch.cuda.synchronize(dev)
+    ev0 = task.evals
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -158,6 +207,7 @@ def main():
     torch.cuda.synchronize(dev)
     T = time.perf_counter() - t0
     kernel_ms = out.kernel_ms
+    evals = task.evals - ev0
     if dist is not None:
         t = torch.tensor([T, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -166,11 +216,37 @@ def main():
     value = total_chains * K / T
 
     spl = args.spl if args.spl >= 0 else 0
-    nbytes, launches = algorithmic_bytes(d, C, K, burnin, args.thinning, spl, grad_sampler)
-    avg_launch_s = kernel_ms * 1e-3 / launches
-    achieved = nbytes / launches / avg_launch_s / 1e9
+    launches = 1 if spl == 0 else -(-K // spl)
+    avg_launch_s = kernel_ms * 1e-3 / launches          # HIP events around the launches, on their stream
+    kname = kernel_name(cfg0, d, args.sampler)
+    if cfg0["model"] == "iso":
+        per_step, per_kept = hbm_bytes_per_unit(d, args.sampler)
+        nbytes = C * K * per_step + C * nkept * per_kept               # per run = per launch x launches
+        achieved = nbytes / launches / avg_launch_s / 1e9
+        moved = (launches * C * (16 * d + 16) + C * nkept * per_kept) / launches / avg_launch_s / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname, "launches": launches,
+                "avg_launch_ms": avg_launch_s * 1e3,
+                "algorithmic_bytes_per_launch": nbytes / launches,
+                "units_per_launch": C * K / launches,
+                "bytes_per_unit": {"chain_step": per_step, "kept_chain_step": per_kept},
+                "state_resident_GBps": moved,
+                "note": "units = chain-steps; the fused kernel keeps chain state in VGPRs across the launch's "
+                        "steps, so HBM moves state once per launch (state_resident_GBps) and the kernel is "
+                        "fp64-VALU bound (DESIGN.md §5)"}
+    else:
+        flop_per_eval = 4.0 * cfg0["n"] * d                           # eta = X beta, then X^T r
+        flops = flop_per_eval * evals
+        achieved = flops / launches / avg_launch_s / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None, "kernel": kname, "launches": launches,
+                "avg_launch_ms": avg_launch_s * 1e3, "flop_per_eval": flop_per_eval,
+                "evals_per_launch": evals / launches,
+                "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
+                        "device); 4 n d fp64 flop each (SURVEY.md §8(d))"}
     line = {
-        "metric": "MCMC steps*chains/sec (1M chains, d=32)",
+        "metric": "MCMC steps*chains/sec (1M chains, d=32)" if args.config == "metric"
+        else f"MCMC steps*chains/sec ({cfg0['desc'].split(':')[0]})",
         "value": value,
         "unit": "chain-steps/s",
         "n_gpus": world,
@@ -181,23 +257,21 @@ def main():
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (model init ones(d); Philox4x32-10 stream, seed 1)",
+        "data": "synthetic (chains start at model.init; Philox4x32-10 streams, seed 1"
+                + ("; regression data from numpy Philox, key 0x5EED)" if cfg0["model"] != "iso" else ")"),
         "config": {
-            "workload": f"{args.config}: iso-Normal -dot(v,v) d={d}, {type(sampler).__name__}, "
-                        f"SerialMC(steps={K}, burnin={burnin}, thinning={args.thinning}), {C} chains/GPU",
+            "workload": f"{args.config}: {cfg0['desc']}; SerialMC(steps={K}, burnin={burnin}, "
+                        f"thinning={args.thinning}), {C} chains/GPU, {type(sampler).__name__}",
             "d": d, "chains_per_gpu": C, "global_chains": total_chains, "sampler": args.sampler,
             "burnin": burnin, "thinning": args.thinning, "kept_per_chain": nkept,
-            "steps_per_launch": spl, "parallelism": f"chains sharded over {world} GPU(s), no collective in loop",
+            "steps_per_launch": spl, "evals": evals,
+            "parallelism": f"chains sharded over {world} GPU(s), no collective in the step loop",
         },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": f"{'lpc' if d <= 32 else 'wpc'}_{args.sampler}", "launches": launches, "avg_launch_ms": avg_launch_s * 1e3,
-            "algorithmic_bytes_per_launch": nbytes / launches,
-        },
+        "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, model, sampler, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,
+                                            C=4096 if cfg0["model"] == "iso" else 256)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
