@@ -1,0 +1,82 @@
+# MCMCHip.jl -- Julia binding of include/mcmc_hip.h (text only: this image has no Julia; see INTEGRATION.md)
+module MCMCHip
+const lib = "libmcmc_hip"          # on LD_LIBRARY_PATH, or an absolute path to mcmchip/libmcmc_hip.so
+
+# ---- structs: field order and types mirror include/mcmc_hip.h exactly (isbits, C layout)
+struct ModelDesc                   # mcmc_model_desc
+    kind::Int32; has_gradient::Int32; d::Int64
+    init::Ptr{Float64}; scale::Ptr{Float64}
+    mu::Float64; sigma::Float64; prior_sigma::Float64; noise_sigma::Float64; link_sign::Float64
+    n::Int64; X::Ptr{Float64}; Y::Ptr{Float64}
+end
+struct SamplerCfg                  # mcmc_sampler_cfg
+    kind::Int32; scale::Float64; drift_step::Float64; n_leaps::Int64; leap_step::Float64
+    rate::Float64; len::Float64; shrinkage::Float64; t0::Float64; step::Float64
+    tuner::Int32; adapt_step::Int64; max_step::Int64; target_path::Float64; target_rate::Float64
+    max_leaps::Int64
+end
+struct RunnerCfg; burnin::Int64; thinning::Int64; len::Int64; end
+mutable struct Outputs             # mcmc_outputs (mutable: the library writes runtime_s, kernel_ms, nkept)
+    samples::Ptr{Float64}; gradients::Ptr{Float64}; accept_bits::Ptr{UInt64}
+    final_x::Ptr{Float64}; final_lp::Ptr{Float64}; on_device::Int32
+    runtime_s::Float64; kernel_ms::Float64; nkept::Int64
+end
+
+const MODEL_ISO_NORMAL_DOT, MODEL_NORMAL_DSL, MODEL_LOGISTIC, MODEL_LINEAR = 1, 2, 3, 4
+const RWM_K, MALA_K, HMC_K, HMCDA_K = 1, 2, 3, 4
+
+check(st) = st == 0 ? nothing :
+    error(unsafe_string(ccall((:mcmc_last_error, lib), Cstring, ())))   # reference @assert text
+
+function context(device::Integer = 0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:mcmc_ctx_create, lib), Cint, (Cint, Ptr{Ptr{Cvoid}}), device, h))
+    h[]
+end
+
+# model(v -> -dot(v,v), grad = v -> -2v, init = ...)   (README.md:60-63)
+function isonormal_model(ctx, init::Vector{Float64}; scale = ones(length(init)))
+    desc = ModelDesc(MODEL_ISO_NORMAL_DOT, 1, length(init), pointer(init), pointer(scale),
+                     0.0, 1.0, 1.0, 1.0, 1.0, 0, C_NULL, C_NULL)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve init scale check(ccall((:mcmc_model_create, lib), Cint,
+        (Ptr{Cvoid}, Ref{ModelDesc}, Ptr{Ptr{Cvoid}}), ctx, desc, h))
+    h[]
+end
+
+# examples/logistic_regression.jl:16-22: X is n x d; the ABI wants row-major [n][d] = Julia X' (column-major)
+function logistic_model(ctx, X::Matrix{Float64}, Y::Vector{Float64}; init = zeros(size(X, 2)))
+    Xr = collect(transpose(X)); scale = ones(size(X, 2))
+    desc = ModelDesc(MODEL_LOGISTIC, 1, size(X, 2), pointer(init), pointer(scale),
+                     0.0, 1.0, 1.0, 1.0, 1.0, size(X, 1), pointer(Xr), pointer(Y))
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve Xr Y init scale check(ccall((:mcmc_model_create, lib), Cint,
+        (Ptr{Cvoid}, Ref{ModelDesc}, Ptr{Ptr{Cvoid}}), ctx, desc, h))
+    h[]
+end
+
+rwm(scale) = SamplerCfg(RWM_K, scale, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+hmc(n, eps) = SamplerCfg(HMC_K, 0, 0, n, eps, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+hmcda(; rate=0.65, len=2., shrinkage=0.05, t0=10., step=0.75) =
+    SamplerCfg(HMCDA_K, 0, 0, 0, 0, rate, len, shrinkage, t0, step, 0, 0, 0, 0, 0, 0)
+
+function chains(model, s::SamplerCfg, nchains; seed = 1, offset = 0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:mcmc_chains_create, lib), Cint,
+        (Ptr{Cvoid}, Ref{SamplerCfg}, Int64, Int64, UInt64, Ptr{Float64}, Ptr{Ptr{Cvoid}}),
+        model, s, nchains, offset, seed, C_NULL, h))
+    h[]
+end
+
+# run_serialmc (SerialMC.jl:37-85): returns samples[nkept][d][C] (Julia: Array{Float64,3} of size (C, d, nkept))
+function run_serialmc(ch, d, C; steps, burnin = 0, thinning = 1)
+    r = (burnin+1):thinning:steps
+    smp = Array{Float64}(undef, C, d, length(r))
+    bits = zeros(UInt64, cld(C, 64), length(r))
+    out = Outputs(pointer(smp), C_NULL, pointer(bits), C_NULL, C_NULL, 0, 0.0, 0.0, 0)
+    GC.@preserve smp bits check(ccall((:mcmc_run_serialmc, lib), Cint,
+        (Ptr{Cvoid}, Ref{RunnerCfg}, Ref{Outputs}), ch, RunnerCfg(burnin, thinning, steps), out))
+    accept = [(bits[fld(c, 64) + 1, j] >> (c % 64)) & 1 == 1 for c in 0:C-1, j in 1:length(r)]
+    smp, accept, out.runtime_s
+end
+end # module
