@@ -215,6 +215,23 @@ def main():
     total_chains = C * world
     value = total_chains * K / T
 
+    # ESS/sec: sum over chains of min over parameters of the IMSE ESS of the kept
+    # samples, per second of sampling; computed on the device after the timed region, timed apart
+    ess_line = None
+    if nkept >= 4:
+        torch.cuda.synchronize(dev)
+        te = time.perf_counter()
+        ess = mc.stats.ess_device(samples, "imse")
+        ess_min_sum = ess.min(dim=0).values.sum()
+        torch.cuda.synchronize(dev)
+        ess_s = time.perf_counter() - te
+        if dist is not None:
+            dist.all_reduce(ess_min_sum, op=dist.ReduceOp.SUM)
+        ess_line = {"ess_per_sec": float(ess_min_sum) / T, "vtype": "imse", "kept_per_chain": nkept,
+                    "sum_min_ess": float(ess_min_sum), "ess_compute_s": ess_s,
+                    "note": "sum_c min_j ESS_cj (ess.jl:6-10, Geyer IMSE) / sampling seconds; ESS on the GPU "
+                            "(kernels/stats.hip), outside the timed region"}
+
     spl = args.spl if args.spl >= 0 else 0
     launches = 1 if spl == 0 else -(-K // spl)
     avg_launch_s = kernel_ms * 1e-3 / launches          # HIP events around the launches, on their stream
@@ -268,6 +285,7 @@ def main():
             "parallelism": f"chains sharded over {world} GPU(s), no collective in the step loop",
         },
         "roofline": roof,
+        "ess": ess_line,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,

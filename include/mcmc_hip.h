@@ -173,6 +173,16 @@ int mcmc_chains_set_store_gradients(mcmc_chains* chains, int32_t store);
 /* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
 int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);
 
+/* ---- output analysis (src/stats/ess.jl:6-10, var.jl:7-117) ----
+ * Effective sample size n * var_iid / var_vtype of every (parameter j, chain c) series of
+ * samples [nkept][d][nchains] (the mcmc_outputs layout).  vtype: MCMC_VAR_IMSE (Geyer initial
+ * monotone sequence), MCMC_VAR_IPSE (initial positive sequence), MCMC_VAR_BM (batch means of
+ * `batchlen`).  maxlag <= 0 -> nkept - 1.  Outputs ess[j][c] and optionally var[j][c] (the vtype
+ * variance of the mean).  on_device != 0: every pointer is device memory on ctx's GPU. */
+enum { MCMC_VAR_IMSE = 1, MCMC_VAR_IPSE = 2, MCMC_VAR_BM = 3 };
+int mcmc_stats_ess(mcmc_ctx* ctx, const double* samples, int64_t nkept, int64_t d, int64_t nchains, int32_t vtype,
+                   int64_t maxlag, int64_t batchlen, int32_t on_device, double* ess, double* var);
+
 /* ---- diagnostics used by the parity tests: evaluate the build's deterministic
  *      math on the device.  op: 0 log, 1 exp, 2 sin2pi, 3 cos2pi,
  *      4 sqrt, 5 div(x, y), 6 normals (x = block counters). ---- */

@@ -29,6 +29,9 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_glm_max_d();
+// effective sample size of every (parameter, chain) series of samples [n][d][C] (stats.hip)
+hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t C, int32_t vtype, int64_t maxlag,
+                           int64_t batchlen, double* ess, double* var, hipStream_t st);
 // padded covariate row length the regression kernels read (X_pad is [n_pad][d_pad])
 int mcmc_glm_d_pad(int d);
 

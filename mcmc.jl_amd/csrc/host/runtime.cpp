@@ -780,6 +780,47 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
 }
 
 // ------------------------------------------------------------------ debug probes
+extern "C" int mcmc_stats_ess(mcmc_ctx* ctx, const double* samples, int64_t nkept, int64_t d, int64_t nchains,
+                              int32_t vtype, int64_t maxlag, int64_t batchlen, int32_t on_device, double* ess,
+                              double* var) {
+    if (!ctx || !samples || !ess) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    if (vtype != MCMC_VAR_IMSE && vtype != MCMC_VAR_IPSE && vtype != MCMC_VAR_BM)       // ess.jl:7
+        return fail(MCMC_E_INVALID_ARG, "Unknown ESS type " + std::to_string(vtype));
+    if (nkept < 2 || d <= 0 || nchains <= 0) return fail(MCMC_E_INVALID_ARG, "need nkept >= 2, d > 0, nchains > 0");
+    if (d > 65535) return fail(MCMC_E_UNSUPPORTED, "d > 65535");
+    if (maxlag <= 0) maxlag = nkept - 1;
+    if (maxlag > nkept - 1) return fail(MCMC_E_INVALID_ARG, "maxlag should be < nkept");
+    if (vtype == MCMC_VAR_BM && !(batchlen > 0 && nkept / batchlen > 1))                   // var.jl:22
+        return fail(MCMC_E_INVALID_ARG, "Choose batch size such that the number of batches is greather than one");
+    if (int r = set_device(ctx)) return r;
+    hipStream_t st = ctx->stream;
+    const size_t ns = (size_t)nkept * (size_t)d * (size_t)nchains, no = (size_t)d * (size_t)nchains;
+    const double* ds = samples;
+    double *dsb = nullptr, *de = ess, *dv = var;
+    int rc = MCMC_OK;
+    do {
+        if (!on_device) {
+            if ((rc = dmalloc(&dsb, ns))) break;
+            if ((rc = dmalloc(&de, no))) break;
+            if (var && (rc = dmalloc(&dv, no))) break;
+            if (h2d(ctx, dsb, samples, ns * 8) != hipSuccess) { rc = fail(MCMC_E_HIP, "samples upload failed"); break; }
+            ds = dsb;
+        }
+        hipError_t e = mcmc_launch_ess(ds, nkept, d, nchains, vtype, maxlag, batchlen, de, dv, st);
+        if (e == hipSuccess && !on_device) e = d2h(ctx, ess, de, no * 8);
+        if (e == hipSuccess && !on_device && var) e = d2h(ctx, var, dv, no * 8);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("ess: ") + hipGetErrorString(e));
+    } while (0);
+    if (!on_device) {
+        (void)hipStreamSynchronize(st);
+        dfree(dsb);
+        dfree(de);
+        dfree(dv);
+    }
+    return rc;
+}
+
 extern "C" int mcmc_debug_detmath(mcmc_ctx* ctx, int op, int64_t n, const double* x, const double* y, double* out) {
     if (!ctx || !x || !out || n <= 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
     if (int r = set_device(ctx)) return r;

@@ -31,6 +31,10 @@ SAMPLER_MALA = 2
 SAMPLER_HMC = 3
 SAMPLER_HMCDA = 4
 
+VAR_IMSE = 1
+VAR_IPSE = 2
+VAR_BM = 3
+
 EXPORTED_SYMBOLS = (
     "mcmc_last_error", "mcmc_abi_version", "mcmc_device_count",
     "mcmc_ctx_create", "mcmc_ctx_destroy", "mcmc_ctx_synchronize",
@@ -38,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_sampler_validate", "mcmc_runner_validate",
     "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done", "mcmc_chains_evals",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients",
-    "mcmc_run_serialmc", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
+    "mcmc_run_serialmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
 )
 
 
@@ -123,6 +127,8 @@ def load() -> ct.CDLL:
         "mcmc_chains_set_steps_per_launch": (ct.c_int, [P, i64]),
         "mcmc_chains_set_store_gradients": (ct.c_int, [P, i32]),
         "mcmc_run_serialmc": (ct.c_int, [P, ct.POINTER(RunnerCfg), ct.POINTER(Outputs)]),
+        "mcmc_stats_ess": (ct.c_int, [P, ct.c_void_p, i64, i64, i64, i32, i64, i64, i32, ct.c_void_p,
+                                      ct.c_void_p]),
         "mcmc_debug_detmath": (ct.c_int, [P, ct.c_int, i64, dp, dp, dp]),
         "mcmc_debug_philox": (ct.c_int, [P, i64, ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32),
                                          ct.POINTER(ct.c_uint32)]),

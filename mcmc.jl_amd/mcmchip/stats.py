@@ -17,10 +17,12 @@ StatsBase is not vendored and has no fixture).
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import numpy as np
 
 __all__ = ["acceptance", "mean", "mcvar_iid", "mcvar_bm", "mcvar_imse", "mcvar_ipse", "var", "ess", "actime",
-           "autocov"]
+           "autocov", "ess_device", "ess_per_sec"]
 
 
 def _samples(c) -> np.ndarray:
@@ -126,3 +128,46 @@ def actime(c, vtype: str = "imse", **kw) -> np.ndarray:
     if vt not in ("bm", "imse", "ipse"):
         raise AssertionError(f"Unknown integrated autocorrelation time type {vtype}")
     return var(c, vt, **kw) / var(c, "iid")
+
+
+_VT = {"imse": 1, "ipse": 2, "bm": 3}
+
+
+def ess_device(c, vtype: str = "imse", maxlag: Optional[int] = None, batchlen: int = 100, device: int = 0,
+               return_var: bool = False):
+    """ESS of every (chain, parameter) series on the GPU (kernels/stats.hip; ess.jl:6-10).
+
+    `c` is an MCMCChain (host samples; returns numpy [nchains, d] like `ess`) or a device tensor
+    [nkept, d, nchains] in the C-ABI layout (returns a device tensor [d, nchains], nothing crosses PCIe)."""
+    import ctypes as ct
+    from . import _lib
+    from .api import _ctx
+    vt = vtype.lstrip(":")
+    if vt not in _VT:
+        raise AssertionError(f"Unknown ESS type {vtype}")
+    lib = _lib.load()
+    ml = 0 if maxlag is None else int(maxlag)
+    if hasattr(c, "data_ptr"):                                   # torch device tensor
+        import torch
+        if c.dim() != 3 or c.dtype != torch.float64 or not c.is_contiguous():
+            raise ValueError("expected a contiguous float64 tensor [nkept, d, nchains]")
+        n, d, C = c.shape
+        e = torch.empty((d, C), dtype=torch.float64, device=c.device)
+        v = torch.empty((d, C), dtype=torch.float64, device=c.device) if return_var else None
+        _lib.check(lib.mcmc_stats_ess(_ctx(c.device.index or 0), c.data_ptr(), n, d, C, _VT[vt], ml, batchlen, 1,
+                                      e.data_ptr(), v.data_ptr() if v is not None else None))
+        return (e, v) if return_var else e
+    s = np.ascontiguousarray(c._samples if hasattr(c, "_samples") else c, dtype=np.float64)
+    n, d, C = s.shape
+    e = np.empty((d, C))
+    v = np.empty((d, C)) if return_var else None
+    _lib.check(lib.mcmc_stats_ess(_ctx(device), s.ctypes.data, n, d, C, _VT[vt], ml, batchlen, 0, e.ctypes.data,
+                                  v.ctypes.data if v is not None else None))
+    return (e.T.copy(), v.T.copy()) if return_var else e.T.copy()
+
+
+def ess_per_sec(ess_dc, seconds: float) -> float:
+    """sum over chains of min over parameters of ESS, per sampling second."""
+    m = ess_dc.min(dim=0).values.sum().item() if hasattr(ess_dc, "min") and hasattr(ess_dc, "dim") \
+        else float(np.min(ess_dc, axis=0).sum())
+    return m / seconds

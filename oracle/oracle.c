@@ -592,3 +592,79 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
 void orc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
     for (int64_t i = 0; i < n; ++i) orc_philox4x32_10(ctr + 4 * i, key + 2 * i, out + 4 * i);
 }
+
+/* ------------------------------------------------------------ output analysis
+ * Effective sample size of every (parameter j, chain c) series of samples [n][d][C]
+ * (ess.jl:6-10): n * var_iid / var_vtype with var_iid = var(x)/n (var.jl:7-8), and
+ * vtype 1 = Geyer IMSE (var.jl:45-75), 2 = IPSE (var.jl:95-117), 3 = batch means (var.jl:20-27).
+ * Autocovariances as StatsBase acf(x, lags, correlation=false): sum_t z_t z_{t+k} / n.
+ * Sums left to right, multiply then add -- the order kernels/stats.hip uses. */
+static double orc_ess_one(const double* x, size_t stride, int64_t n, int vtype, int64_t maxlag, int64_t bl,
+                          double* var_out) {
+    const double nd = (double)n;
+    double sum = 0.0;
+    for (int64_t t = 0; t < n; ++t) sum = sum + x[(size_t)t * stride];
+    const double mean = sum / nd;
+    double ss = 0.0;
+    for (int64_t t = 0; t < n; ++t) {
+        const double z = x[(size_t)t * stride] - mean;
+        ss = ss + z * z;
+    }
+    const double var_iid = (ss / (nd - 1.0)) / nd;
+    double var_v;
+    if (vtype == 3) {
+        const int64_t nb = n / bl;
+        double bsum = 0.0;
+        for (int64_t b = 0; b < nb; ++b) {
+            double s = 0.0;
+            for (int64_t t = b * bl; t < (b + 1) * bl; ++t) s = s + x[(size_t)t * stride];
+            bsum = bsum + s / (double)bl;
+        }
+        const double bmean = bsum / (double)nb;
+        double bss = 0.0;
+        for (int64_t b = 0; b < nb; ++b) {
+            double s = 0.0;
+            for (int64_t t = b * bl; t < (b + 1) * bl; ++t) s = s + x[(size_t)t * stride];
+            const double e = s / (double)bl - bmean;
+            bss = bss + e * e;
+        }
+        var_v = ((double)bl * (bss / (double)(nb - 1))) / (double)(nb * bl);
+    } else {
+        const int64_t k = (maxlag - 1) >= 0 ? (maxlag - 1) / 2 : -1;    /* floor((maxlag-1)/2) */
+        const double acv0 = ss / nd;
+        double gsum = 0.0, prev = 0.0;
+        for (int64_t j = 0; j <= k; ++j) {
+            double acv[2];
+            for (int h = 0; h < 2; ++h) {
+                const int64_t lag = 2 * j + h;
+                if (lag == 0) {
+                    acv[h] = acv0;
+                    continue;
+                }
+                double s = 0.0;
+                for (int64_t t = 0; t + lag < n; ++t)
+                    s = s + (x[(size_t)t * stride] - mean) * (x[(size_t)(t + lag) * stride] - mean);
+                acv[h] = s / nd;
+            }
+            double g = acv[0] + acv[1];
+            if (g <= 0.0) break;                                       /* m = j */
+            if (vtype == 1 && j > 0 && g > prev) g = prev;             /* initial monotone sequence */
+            prev = g;
+            gsum = gsum + g;
+        }
+        var_v = (-acv0 + 2.0 * gsum) / nd;
+    }
+    if (var_out) *var_out = var_v;
+    return (nd * var_iid) / var_v;
+}
+
+void orc_ess(const double* samples, int64_t n, int64_t d, int64_t C, int vtype, int64_t maxlag, int64_t batchlen,
+             double* ess, double* var) {
+    if (maxlag <= 0) maxlag = n - 1;
+#pragma omp parallel for schedule(static)
+    for (int64_t o = 0; o < d * C; ++o) {
+        const int64_t j = o / C, c = o % C;
+        ess[o] = orc_ess_one(samples + (size_t)j * C + c, (size_t)d * C, n, vtype, maxlag, batchlen,
+                             var ? var + o : NULL);
+    }
+}

@@ -178,6 +178,19 @@ def detmath(op, x, y=None):
     return out
 
 
+def ess(samples, vtype=1, maxlag=0, batchlen=100):
+    """orc_ess: samples [nkept][d][C] -> (ess [d][C], var [d][C]); vtype 1 imse, 2 ipse, 3 bm."""
+    s = np.ascontiguousarray(samples, dtype=np.float64)
+    n, d, C = s.shape
+    e = np.empty((d, C))
+    v = np.empty((d, C))
+    L = lib()
+    L.orc_ess.restype = None
+    L.orc_ess.argtypes = [D, ct.c_int64, ct.c_int64, ct.c_int64, ct.c_int, ct.c_int64, ct.c_int64, D, D]
+    L.orc_ess(_d(s), n, d, C, vtype, maxlag, batchlen, _d(e), _d(v))
+    return e, v
+
+
 def philox(ctr, key):
     ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
     key = np.ascontiguousarray(key, dtype=np.uint32).reshape(-1, 2)

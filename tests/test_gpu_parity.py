@@ -328,3 +328,34 @@ def test_model_released_before_its_chains(gpu):
     s, g, acc = oc.run(r)
     assert_parity(ch, s, g, acc, "hmc")
     del t, ch                               # last chains gone: the model is freed now
+
+
+@pytest.mark.parametrize("vtype,name", [(1, "imse"), (2, "ipse"), (3, "bm")])
+@pytest.mark.parametrize("n", [90, 300])                  # LDS-staged series / global re-reads
+def test_device_ess_bitwise(gpu, vtype, name, n):
+    import torch
+    rng = np.random.default_rng(n + vtype)
+    d, C = 3, 130
+    e = rng.normal(size=(n, d, C))
+    x = np.zeros_like(e)
+    x[0] = e[0]
+    for t in range(1, n):
+        x[t] = 0.6 * x[t - 1] + e[t]
+    ref, vref = orc.ess(x, vtype, 0, 20)
+    chain = type("Chain", (), {})()
+    chain._samples = x
+    got, v = mc.stats.ess_device(chain, name, batchlen=20, return_var=True)
+    assert np.array_equal(got.T, ref) and np.array_equal(v.T, vref)
+    xt = torch.from_numpy(x).cuda()
+    got_d = mc.stats.ess_device(xt, name, batchlen=20)     # device pointers, no PCIe
+    assert np.array_equal(got_d.cpu().numpy(), ref)
+
+
+def test_device_ess_of_a_run(gpu):
+    m = _model("iso", 4)
+    ch = mc.run(m * mc.HMC(0.75) * mc.SerialMC(steps=600, burnin=100), nchains=70, seed=3)
+    ref, _ = orc.ess(ch._samples, 1)
+    assert np.array_equal(mc.stats.ess_device(ch), ref.T)
+    np.testing.assert_allclose(mc.stats.ess_device(ch), mc.stats.ess(ch), rtol=1e-9)
+    with pytest.raises(mc.MCMCError, match="greather than one"):
+        mc.stats.ess_device(ch, "bm", batchlen=400)

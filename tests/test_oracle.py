@@ -368,3 +368,25 @@ def test_mala_logistic_recovers_posterior_mean():
     sd = np.sqrt(np.diag(np.linalg.inv(-H)))
     assert np.all(np.abs(post - b) < 0.25 * sd + 0.02)
     assert 0.2 < acc.mean() < 0.99
+
+
+@pytest.mark.parametrize("vtype,name", [(1, "imse"), (2, "ipse"), (3, "bm")])
+@pytest.mark.parametrize("phi", [0.0, 0.7, 0.95, -0.5])
+def test_oracle_ess_matches_numpy_stats(vtype, name, phi):
+    """orc_ess restates ess.jl / var.jl; numpy stats.py (FFT autocovariances) agrees to rounding."""
+    import mcmchip as mc
+    rng = np.random.default_rng(5)
+    n, d, C = 180, 2, 7
+    e = rng.normal(size=(n, d, C))
+    x = np.zeros_like(e)
+    x[0] = e[0]
+    for t in range(1, n):
+        x[t] = phi * x[t - 1] + e[t]
+    eo, vo = orc.ess(x, vtype, 0, 30)
+    chain = type("Chain", (), {})()
+    chain.samples = np.transpose(x, (2, 0, 1))
+    kw = {"batchlen": 30} if name == "bm" else {}
+    en = mc.stats.ess(chain, name, **kw)
+    np.testing.assert_allclose(eo.T, en, rtol=1e-10)
+    if phi == 0.7 and name == "imse":            # AR(1): ESS ~ n (1 - phi) / (1 + phi)
+        assert abs(np.mean(eo) / (n * 0.3 / 1.7) - 1) < 0.35
