@@ -129,11 +129,14 @@ def cpu_baseline(model, sampler, seconds, C=4096):
     import mcmchip as mc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
-    steps = 4
-    t0 = time.perf_counter()
-    oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
-    oc.run(mc.SerialMC(steps=steps, burnin=1, thinning=1), nthreads=threads)
-    dt = time.perf_counter() - t0
+    # calibrate on a short run (state set-up excluded), then size the timed sample to ~`seconds`
+    steps, dt = 2, 0.0
+    while dt < 0.5 and steps < 1 << 16:
+        steps *= 4
+        oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
+        t0 = time.perf_counter()
+        oc.run(mc.SerialMC(steps=steps, burnin=1, thinning=1), nthreads=threads)
+        dt = time.perf_counter() - t0
     rate = C * steps / dt
     steps2 = max(steps, int(rate * seconds / C))
     oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
