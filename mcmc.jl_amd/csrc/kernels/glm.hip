@@ -87,6 +87,7 @@ struct GlmLds {
     double* Y;
     double* part;
     double* scal;
+    double* rbuf;     // [4 tiles][4 r][64 lanes]: residual weights of a tile, exchanged between slice waves
     int* iscr;
 };
 
@@ -96,12 +97,13 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     L.Y = L.X + 16 * a.g.lds_stride;
     L.part = L.Y + 16;
     L.scal = L.part + kGlmMaxWaves * 64 * 4;
-    L.iscr = (int*)(L.scal + kGlmMaxWaves * 16);
+    L.rbuf = L.scal + kGlmMaxWaves * 16;
+    L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
     return L;
 }
 
 size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(16 * g.lds_stride + 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4) * 8;
+    return (size_t)(16 * g.lds_stride + 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4 * 4 * 64 + 4) * 8;
 }
 
 // sum of a per-chain quantity held as 4 quarter partials per wave and NW slice partials:
@@ -145,6 +147,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     const double sgn = M.link_sign;
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = logistic ? 0.0 : det_log(sn);
+    const double isn = 1.0 / sn, is2n = 1.0 / s2n;
     if (GRAD) {
 #pragma unroll
         for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -198,41 +201,55 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
                 eta = __builtin_amdgcn_mfma_f64_16x16x4f64(av, x[slot], eta, 0, 0, 0);
             }
         }
+        // Elementwise part, split over the slice waves: wave slice s owns observation rows r in
+        // [s*RPW, (s+1)*RPW) of the tile (obs 16t + q + 4r for lane (q, cl)); with NW = 8 slices 4..7 own
+        // none.  Its eta is the slices' partials added left to right.
+        constexpr int RPW = NW >= 4 ? 1 : 4 / NW;
+        const int r0 = p.slice * RPW;
         if (NW > 1) {
             double* mine = L.part + (p.wave * 64 + p.lane) * 4;
             mine[0] = eta[0]; mine[1] = eta[1]; mine[2] = eta[2]; mine[3] = eta[3];
             __syncthreads();
-            const double* p0 = L.part + ((p.tile * NW) * 64 + p.lane) * 4;
-            eta = f64x4{p0[0], p0[1], p0[2], p0[3]};
-            for (int s = 1; s < NW; ++s) {
-                const double* ps = L.part + ((p.tile * NW + s) * 64 + p.lane) * 4;
-                eta[0] = eta[0] + ps[0]; eta[1] = eta[1] + ps[1];
-                eta[2] = eta[2] + ps[2]; eta[3] = eta[3] + ps[3];
-            }
         }
-        // elementwise: obs 16t + q + 4r for chain cl
         double rv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int rr_ = 0; rr_ < RPW; ++rr_) {
+            const int r = r0 + rr_;
+            if (r >= 4) break;
+            double e;
+            if (NW > 1) {
+                e = L.part[((p.tile * NW) * 64 + p.lane) * 4 + r];
+                for (int sl = 1; sl < NW; ++sl) e = e + L.part[((p.tile * NW + sl) * 64 + p.lane) * 4 + r];
+            } else {
+                e = eta[r];
+            }
             const int64_t obs = t * 16 + p.q + 4 * r;
             const double y = L.Y[p.q + 4 * r];
-            double term, rr;
+            double term, w;
             if (logistic) {
-                const double tt = det_exp(-(sgn * eta[r]));             // prob = 1/(1+exp(-X*vars))
-                const double u = 1.0 + tt;
-                const double pr = 1.0 / u;
+                const double tt = det_exp(-(sgn * e));                  // prob = 1/(1+exp(-X*vars))
+                const double pr = 1.0 / (1.0 + tt);
                 term = (y >= 0.5) ? det_log(pr) : det_log(1.0 - pr);   // Y ~ Bernoulli(prob)
-                const double dprob = 1.0 / ((pr - 1.0) + y);            // MCMCDerivRules.jl:111
-                rr = sgn * ((dprob * tt) / (u * u));
+                w = sgn * (y - pr);                                     // MCMCDerivRules.jl:111 chain, closed form
             } else {
-                const double resid = y - eta[r];                        // resid = Y - X*vars
-                const double z = resid / sn;
+                const double resid = y - e;                             // resid = Y - X*vars
+                const double z = resid * isn;
                 term = -0.5 * (z * z + kLog2Pi) - logsn;                // resid ~ Normal(0, sn)
-                rr = resid / s2n;
+                w = resid * is2n;
             }
             const bool in = obs < M.n;
             if (in) lik_part = lik_part + term;
-            rv[r] = in ? rr : 0.0;
+            rv[(NW > 1) ? rr_ : r] = in ? w : 0.0;
+        }
+        if (NW > 1) {
+            // publish the owned rows' weights, then every slice wave reads all four for its G product
+            double* rb = L.rbuf + p.tile * 256;
+#pragma unroll
+            for (int rr_ = 0; rr_ < RPW; ++rr_)
+                if (r0 + rr_ < 4) rb[(r0 + rr_) * 64 + p.lane] = rv[rr_];
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rv[r] = rb[r * 64 + p.lane];
         }
         if (GRAD) {
             // G tile T, k-slice kk': A[i][k] = X[obs 4kk'+q][coord base+16T+4(i&3)+(i>>2)], i = cl
@@ -249,9 +266,8 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             }
         }
     }
-    // likelihood: quarter combine only (identical in every slice wave)
-    double lik = lik_part + __shfl_xor(lik_part, 32, 64);
-    lik = lik + __shfl_xor(lik, 16, 64);
+    // likelihood: quarter combine, then slices left to right (each slice wave owns some rows)
+    const double lik = glm_sum(a, p, L, lik_part);
     // prior vars ~ Normal(0, sp) over own coordinates
     const double sp = M.prior_sigma, s2p = sp * sp, logsp = det_log(sp);
     double pp = 0.0;

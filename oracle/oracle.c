@@ -191,9 +191,15 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
     for (int k = 0; k < dp; ++k) { xp[k] = k < d ? x[k] : 0.0; G[k] = 0.0; }
     const double sp = m->prior_sigma, s2p = sp * sp, logsp = orc_log(sp);
     const double sn = m->noise_sigma, s2n = sn * sn, logsn = orc_log(sn);
+    const double isn = 1.0 / sn, is2n = 1.0 / s2n;
     const double sgn = m->link_sign;
-    /* likelihood: lane (chain, q) accumulates obs 16t + q + 4r in (t, r) order */
-    double lik_part[4] = {0.0, 0.0, 0.0, 0.0};
+    /* likelihood: obs i = 16t + q + 4r belongs to slice wave s = r / RPW (RPW = 4/NW rows per wave, 1 for
+       NW >= 4; with NW = 8 slices 4..7 own none); lane (chain, q) of that wave accumulates its obs in (t, r)
+       order */
+    const int rpw = geo.nw >= 4 ? 1 : 4 / geo.nw;
+    double lik_part[8][4];
+    for (int s = 0; s < 8; ++s)
+        for (int q = 0; q < 4; ++q) lik_part[s][q] = 0.0;
     for (int64_t i = 0; i < geo.n_pad; ++i) {
         const double* Xi = (i < m->n) ? m->X + (size_t)i * d : NULL;
         /* eta_i: per slice an fma chain over (mm, e, q), slices added left to right */
@@ -214,19 +220,20 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
             const double y = m->Y[i];
             if (m->kind == ORC_MODEL_LINEAR) {
                 double resid = y - eta;                           /* resid = Y - X*vars */
-                double z = resid / sn;
+                double z = resid * isn;
                 term = -0.5 * (z * z + ORC_LOG2PI) - logsn;       /* resid ~ Normal(0, sn) */
-                r = resid / s2n;                                  /* -d/dresid, MCMCDerivRules.jl:57 */
+                r = resid * is2n;                                 /* -d/dresid, MCMCDerivRules.jl:57 */
             } else {
                 double tt = orc_exp(-(sgn * eta));                /* prob = 1/(1+exp(-X*vars)) */
-                double u = 1.0 + tt;
-                double p = 1.0 / u;
+                double p = 1.0 / (1.0 + tt);
                 term = (y >= 0.5) ? orc_log(p) : orc_log(1.0 - p);   /* Y ~ Bernoulli(prob) */
-                double dprob = 1.0 / ((p - 1.0) + y);              /* dd1 += 1/(d.p1 - 1 + x) (MCMCDerivRules.jl:111) */
-                r = sgn * ((dprob * tt) / (u * u));                /* dprob/deta = s t / u^2 */
+                /* d/deta of the Bernoulli term: the rule dd1 += 1/(p - 1 + y) (MCMCDerivRules.jl:111) times
+                   dprob/deta = s t / (1+t)^2 is s (y - p) for y in {0, 1}; the closed form is used */
+                r = sgn * (y - p);
             }
-            const int q = (int)(i & 3);
-            lik_part[q] = lik_part[q] + term;
+            const int q = (int)(i & 3), rr = (int)((i & 15) >> 2);
+            double* lp_ = lik_part[rr / rpw];
+            lp_[q] = lp_[q] + term;
         }
         /* G_k = sum_i X[i][k] r_i, fma chain over obs (padded obs: X = 0, r = 0) */
         for (int k = 0; k < dp; ++k) {
@@ -234,7 +241,11 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
             G[k] = fma(xik, r, G[k]);
         }
     }
-    const double lik = (lik_part[0] + lik_part[2]) + (lik_part[1] + lik_part[3]);
+    double lik = 0.0;
+    for (int s = 0; s < geo.nw; ++s) {
+        const double w = (lik_part[s][0] + lik_part[s][2]) + (lik_part[s][1] + lik_part[s][3]);
+        lik = s == 0 ? w : lik + w;
+    }
     for (int k = 0; k < dp; ++k) {
         double z = (xp[k] - 0.0) / sp;
         t[k] = -0.5 * (z * z + ORC_LOG2PI) - logsp;                /* vars ~ Normal(0, sp) */
