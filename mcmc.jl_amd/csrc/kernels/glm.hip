@@ -80,8 +80,8 @@ __device__ __forceinline__ int own_coord(const GlmPos& p, int slot) {
     return p.base + 16 * (slot >> 2) + 4 * p.q + (slot & 3);
 }
 
-// LDS carve-up (doubles): X tile [16][stride] | Y tile [16] | eta partials [4 waves][64][4] |
-// chain scalars [4 waves][16] | int scratch
+// LDS carve-up (doubles): X tiles [2][16][stride] | Y tiles [2][16] | eta partials [8 waves][64][4] |
+// chain scalars [8 waves][16] | residual weights [4 tiles][4][64] | int scratch
 struct GlmLds {
     double* X;
     double* Y;
@@ -94,8 +94,8 @@ struct GlmLds {
 __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     GlmLds L;
     L.X = smem;
-    L.Y = L.X + 16 * a.g.lds_stride;
-    L.part = L.Y + 16;
+    L.Y = L.X + 2 * 16 * a.g.lds_stride;             // X: two tile buffers
+    L.part = L.Y + 2 * 16;
     L.scal = L.part + kGlmMaxWaves * 64 * 4;
     L.rbuf = L.scal + kGlmMaxWaves * 16;
     L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
@@ -103,7 +103,7 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
 }
 
 size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(16 * g.lds_stride + 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4 * 4 * 64 + 4) * 8;
+    return (size_t)(2 * 16 * g.lds_stride + 2 * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4 * 4 * 64 + 4) * 8;
 }
 
 // sum of a per-chain quantity held as 4 quarter partials per wave and NW slice partials:
@@ -154,46 +154,49 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     }
     double lik_part = 0.0;
     const int64_t ntiles = g.n_pad / 16;
-    for (int64_t t = 0; t < ntiles; ++t) {
-        // stage X rows 16t..16t+15 (contiguous, 16 * d_pad doubles) into padded LDS rows: all loads of
-        // the tile are issued before the barrier that retires the previous tile's readers
-        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)t * 16 * g.d_pad);
-        constexpr int kBlk = glm_block<NW>();
-        constexpr int kHalf = 16 * 8 * NM * NW;               // f64x2 per tile (d_pad = 16 NM NW)
-        constexpr int kPer = (kHalf + kBlk - 1) / kBlk;
-        constexpr int kRound = kPer < 8 ? kPer : 8;
-        constexpr int kLgHalfrow = __builtin_ctz(8 * NM * NW);
-        const double ytile = (threadIdx.x < 16) ? M.Y[t * 16 + threadIdx.x] : 0.0;
-        f64x2 buf[kRound];
+    // X rows 16t..16t+15 (contiguous, 16 * d_pad doubles) are staged into padded LDS rows, double
+    // buffered: tile t+1's loads are issued before tile t's compute and written to the other buffer
+    // after it, so one barrier per tile retires both the readers of tile t and the writers of t+1.
+    constexpr int kBlk = glm_block<NW>();
+    constexpr int kHalf = 16 * 8 * NM * NW;                   // f64x2 per tile (d_pad = 16 NM NW)
+    constexpr int kPer = (kHalf + kBlk - 1) / kBlk;           // <= 8 for every built shape
+    constexpr int kLgHalfrow = __builtin_ctz(8 * NM * NW);
+    const int XS = 16 * S;                                    // doubles per LDS X buffer
+    f64x2 buf[kPer];
+    double ytile = 0.0;
+    auto load_tile = [&](int64_t tt) {
+        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * 16 * g.d_pad);
 #pragma unroll
-        for (int j = 0; j < kRound; ++j) {
+        for (int j = 0; j < kPer; ++j) {
             const int i = threadIdx.x + kBlk * j;
             buf[j] = src[i < kHalf ? i : 0];                  // unconditional load: no exec branch
         }
-        __syncthreads();                                      // previous tile's readers are done
+        ytile = (threadIdx.x < 16) ? M.Y[tt * 16 + threadIdx.x] : 0.0;
+    };
+    auto store_tile = [&](int b) {
+        double* Xb = L.X + b * XS;
 #pragma unroll
-        for (int j0 = 0; j0 < kPer; j0 += kRound) {
-            if (j0 > 0) {
-#pragma unroll
-                for (int j = 0; j < kRound; ++j) {
-                    const int i = threadIdx.x + kBlk * (j0 + j);
-                    buf[j] = src[i < kHalf ? i : 0];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kRound; ++j) {
-                const int i = threadIdx.x + kBlk * (j0 + j);
-                if (i < kHalf) {
-                    const int row = i >> kLgHalfrow, col = 2 * (i & ((1 << kLgHalfrow) - 1));
-                    *reinterpret_cast<f64x2*>(&L.X[row * S + col]) = buf[j];
-                }
+        for (int j = 0; j < kPer; ++j) {
+            const int i = threadIdx.x + kBlk * j;
+            if (i < kHalf) {
+                const int row = i >> kLgHalfrow, col = 2 * (i & ((1 << kLgHalfrow) - 1));
+                *reinterpret_cast<f64x2*>(&Xb[row * S + col]) = buf[j];
             }
         }
-        if (threadIdx.x < 16) L.Y[threadIdx.x] = ytile;
-        __syncthreads();
+        if (threadIdx.x < 16) L.Y[b * 16 + threadIdx.x] = ytile;
+    };
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int b = (int)(t & 1);
+        const double* LX = L.X + b * XS;
+        const double* LY = L.Y + b * 16;
+        const bool more = t + 1 < ntiles;
+        if (more) load_tile(t + 1);
         // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e
         f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
-        const double* xrow = L.X + p.cl * S + p.base + 4 * p.q;
+        const double* xrow = LX + p.cl * S + p.base + 4 * p.q;
 #pragma unroll
         for (int slot = 0; slot < (4 * NM); ++slot) {
             if (true) {
@@ -224,7 +227,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
                 e = eta[r];
             }
             const int64_t obs = t * 16 + p.q + 4 * r;
-            const double y = L.Y[p.q + 4 * r];
+            const double y = LY[p.q + 4 * r];
             double term, w;
             if (logistic) {
                 const double tt = det_exp(-(sgn * e));                  // prob = 1/(1+exp(-X*vars))
@@ -253,7 +256,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         }
         if (GRAD) {
             // G tile T, k-slice kk': A[i][k] = X[obs 4kk'+q][coord base+16T+4(i&3)+(i>>2)], i = cl
-            const double* gcol = L.X + p.base + 4 * (p.cl & 3) + (p.cl >> 2);
+            const double* gcol = LX + p.base + 4 * (p.cl & 3) + (p.cl >> 2);
 #pragma unroll
             for (int T = 0; T < NM; ++T) {
                 if (true) {
@@ -265,6 +268,8 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
                 }
             }
         }
+        if (more) store_tile(b ^ 1);                          // the other buffer: its readers finished tile t-1
+        __syncthreads();
     }
     // likelihood: quarter combine, then slices left to right (each slice wave owns some rows)
     const double lik = glm_sum(a, p, L, lik_part);
