@@ -62,6 +62,8 @@ struct StepArgs {
     int64_t burnin, thinning, len;   // runner range (run-local)
     int64_t tuner_burnin;       // runner.burnin as seen by the sampler loop (global i)
     const double* scale;        // [d] model.scale .* sampler.scale (RWM) or model.scale
+    double scale1;              // the common value when every scale[j] is equal (scale_uniform)
+    int32_t scale_uniform;
     double* samples;            // [nkept][d][C]  (NULL: not stored)
     double* grads;              // [nkept][d][C]  (NULL: not stored)
     uint64_t* acc_bits;         // [nkept][nw]

@@ -84,6 +84,8 @@ struct mcmc_chains {
     Layout layout = LAYOUT_LPC;
     ChainState st{};
     double* d_scale_eff = nullptr;   // model.scale .* sampler.scale (RWM.jl:52)
+    double scale1 = 0.0;             // its common value when all coordinates agree
+    int32_t scale_uniform = 0;
     double* d_init_x = nullptr;      // optional per-chain start, [d][C]
     unsigned long long* d_evals = nullptr;   // log-target evaluations since create/reset (all chains)
     int64_t steps_done = 0;
@@ -581,6 +583,10 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     std::vector<double> se(m->scale);
     if (sa.kind == SK_RWM)
         for (auto& v : se) v = v * sa.scale;
+    c->scale1 = se.empty() ? 0.0 : se[0];
+    c->scale_uniform = 1;
+    for (double v : se)
+        if (!(v == c->scale1)) c->scale_uniform = 0;   // bitwise-equal products only (NaN never)
     if (int r = dmalloc(&c->d_scale_eff, (size_t)round_up(d, 256))) return bail(r);
     if (int r = dmalloc(&c->d_evals, 1)) return bail(r);
     if (dzero(ctx, c->d_scale_eff, (size_t)round_up(d, 256) * 8) != hipSuccess ||
@@ -724,6 +730,8 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     s.len = r->len;
     s.tuner_burnin = r->burnin;
     s.scale = c->d_scale_eff;
+    s.scale1 = c->scale1;
+    s.scale_uniform = c->scale_uniform;
 
     s.samples = k_samples;
     s.grads = k_grads;

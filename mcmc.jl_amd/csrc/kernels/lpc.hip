@@ -4,36 +4,45 @@
 
 namespace mcmc {
 
-template <int NB, class M>
-__global__ __launch_bounds__(kBlock) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB>, M>(a); }
-template <int NB, class M>
-__global__ __launch_bounds__(kBlock) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB>, M>(a); }
-template <int NB, class M, bool DA>
-__global__ __launch_bounds__(kBlock) void lpc_hmc(KernelArgs a) { hmc_body<LaneChain<NB>, M, DA>(a); }
+// F: d == 4 NB (LaneChain FULL); US: uniform RWM scale
+template <int NB, bool F, class M, bool US>
+__global__ __launch_bounds__(kBlock) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
+template <int NB, bool F, class M>
+__global__ __launch_bounds__(kBlock) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
+template <int NB, bool F, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void lpc_hmc(KernelArgs a) { hmc_body<LaneChain<NB, F>, M, DA>(a); }
 template <int NB, class M>
 __global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {
     eval_body<LaneChain<NB>, M>(a, xin, lp, g, check);
 }
 
-template <int NB, class M>
+template <int NB, bool F, class M>
 static hipError_t launch_model(const KernelArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
     switch (a.sa.kind) {
-        case SK_RWM: lpc_rwm<NB, M><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_MALA: lpc_mala<NB, M><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_HMC: lpc_hmc<NB, M, false><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_HMCDA: lpc_hmc<NB, M, true><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_RWM:
+            if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            break;
+        case SK_MALA: lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMC: lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMCDA: lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
+template <int NB, bool F>
+static hipError_t launch_nbf(const KernelArgs& a, hipStream_t st) {
+    if (a.m.kind == MK_ISO) return launch_model<NB, F, IsoDot>(a, st);
+    if (a.m.kind == MK_NORMAL) return launch_model<NB, F, NormalDSL>(a, st);
+    return hipErrorInvalidValue;
+}
+
 template <int NB>
 static hipError_t launch_nb(const KernelArgs& a, hipStream_t st) {
-    if (a.m.kind == MK_ISO) return launch_model<NB, IsoDot>(a, st);
-    if (a.m.kind == MK_NORMAL) return launch_model<NB, NormalDSL>(a, st);
-    return hipErrorInvalidValue;
+    return a.s.d == 4 * NB ? launch_nbf<NB, true>(a, st) : launch_nbf<NB, false>(a, st);
 }
 
 template <int NB>
@@ -46,13 +55,7 @@ static hipError_t launch_eval_nb(const KernelArgs& a, const double* xin, double*
     return hipGetLastError();
 }
 
-static int nb_for(int d) {
-    if (d <= 4) return 1;
-    if (d <= 8) return 2;
-    if (d <= 16) return 4;
-    if (d <= 32) return 8;
-    return 0;
-}
+static int nb_for(int d) { return d >= 1 && d <= 32 ? (d + 3) / 4 : 0; }
 
 }  // namespace mcmc
 
@@ -60,7 +63,11 @@ hipError_t mcmc_launch_lpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
     switch (mcmc::nb_for(a.s.d)) {
         case 1: return mcmc::launch_nb<1>(a, st);
         case 2: return mcmc::launch_nb<2>(a, st);
+        case 3: return mcmc::launch_nb<3>(a, st);
         case 4: return mcmc::launch_nb<4>(a, st);
+        case 5: return mcmc::launch_nb<5>(a, st);
+        case 6: return mcmc::launch_nb<6>(a, st);
+        case 7: return mcmc::launch_nb<7>(a, st);
         case 8: return mcmc::launch_nb<8>(a, st);
         default: return hipErrorInvalidValue;
     }
@@ -71,7 +78,11 @@ hipError_t mcmc_launch_lpc_eval(const mcmc::KernelArgs& a, const double* xin, do
     switch (mcmc::nb_for(a.s.d)) {
         case 1: return mcmc::launch_eval_nb<1>(a, xin, lp, g, check, st);
         case 2: return mcmc::launch_eval_nb<2>(a, xin, lp, g, check, st);
+        case 3: return mcmc::launch_eval_nb<3>(a, xin, lp, g, check, st);
         case 4: return mcmc::launch_eval_nb<4>(a, xin, lp, g, check, st);
+        case 5: return mcmc::launch_eval_nb<5>(a, xin, lp, g, check, st);
+        case 6: return mcmc::launch_eval_nb<6>(a, xin, lp, g, check, st);
+        case 7: return mcmc::launch_eval_nb<7>(a, xin, lp, g, check, st);
         case 8: return mcmc::launch_eval_nb<8>(a, xin, lp, g, check, st);
         default: return hipErrorInvalidValue;
     }

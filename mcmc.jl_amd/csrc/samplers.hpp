@@ -33,7 +33,9 @@ namespace mcmc {
 constexpr int kBlock = 256;
 
 // ------------------------------------------------------------------ mappings
-template <int NB_>
+// NB = ceil(d/4).  FULL: d == 4 NB, every register coordinate is a real one -- no validity masks
+// (with a runtime d they are per-coordinate uniform masks, which overflow the SGPR file at NB = 8).
+template <int NB_, bool FULL = false>
 struct LaneChain {
     static constexpr int NB = NB_;
     static constexpr int NC = 4 * NB_;
@@ -46,19 +48,29 @@ struct LaneChain {
         d = s.d;
     }
     __device__ __forceinline__ int coord(int k) const { return k; }
-    __device__ __forceinline__ bool valid(int k) const { return k < d; }
+    // blocks 0..NB-2 are always full (NB = ceil(d/4)); only the last block's coordinates are tested
+    __device__ __forceinline__ bool valid(int k) const { return FULL || k < 4 * (NB - 1) || k < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)b; }
     __device__ __forceinline__ double reduce(double v) const { return v; }
+    // running addresses (see store_kept): no per-coordinate uniform offsets live across the step loop
     __device__ __forceinline__ void load(const double* x, int64_t ld, double (&v)[NC]) const {
-        const int64_t cc = live ? c : 0;
+        const double* p = x + (live ? c : 0);
 #pragma unroll
-        for (int k = 0; k < NC; ++k) v[k] = valid(k) ? x[(size_t)k * ld + cc] : 0.0;
+        for (int k = 0; k < NC; ++k) {
+            v[k] = valid(k) ? *p : 0.0;
+            p += ld;
+            asm volatile("" : "+v"(p));
+        }
     }
     __device__ __forceinline__ void store(double* x, int64_t ld, const double (&v)[NC]) const {
         if (!live) return;
+        double* p = x + c;
 #pragma unroll
-        for (int k = 0; k < NC; ++k)
-            if (valid(k)) x[(size_t)k * ld + c] = v[k];
+        for (int k = 0; k < NC; ++k) {
+            if (valid(k)) *p = v[k];
+            p += ld;
+            asm volatile("" : "+v"(p));
+        }
     }
     __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
     template <class T>
@@ -72,9 +84,15 @@ struct LaneChain {
                                                double* base) const {
         if (base == nullptr || !live) return;
         double* p = base + (size_t)kk * (size_t)d * (size_t)s.C + (size_t)c;
+        const size_t C = (size_t)s.C;
 #pragma unroll
-        for (int k = 0; k < NC; ++k)
-            if (valid(k)) p[(size_t)k * (size_t)s.C] = v[k];
+        for (int k = 0; k < NC; ++k) {
+            if (valid(k)) *p = v[k];
+            p += C;
+            // one running address: otherwise the NC uniform offsets k*C are precomputed and held in
+            // SGPRs across the step loop, spilling the scalar file
+            asm volatile("" : "+v"(p));
+        }
     }
     // add this chain's evaluation count to the launch-wide counter (one atomic per wave)
     __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
@@ -221,7 +239,8 @@ __device__ __forceinline__ double tune_factor(int32_t acc, int32_t prop, double 
 }
 
 // ------------------------------------------------------------------ RWM
-template <class P, class M>
+// US: every coordinate has the same scale (s.scale1), held in one SGPR pair instead of d of them
+template <class P, class M, bool US = false>
 __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     const StepArgs& s = a.s;
     const P p(s);
@@ -231,7 +250,7 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     double x[P::NC], sc[P::NC];
     p.load(a.st.x, s.ld, x);
 #pragma unroll
-    for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? s.scale[p.coord(k)] : 0.0;
+    for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
     double lp = p.load_scalar(a.st.lp);
 
     for (int t = 0; t < s.nsteps; ++t) {
