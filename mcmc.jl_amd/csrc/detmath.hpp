@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bm_log_table.inc"
+
 namespace mcmc {
 
 enum : uint32_t { TAG_NORMAL = 0u, TAG_ACCEPT = 1u, TAG_DATA = 7u };
@@ -159,18 +161,83 @@ __device__ __forceinline__ void det_sincos2pi(double u, double& s_out, double& c
     c_out = (qi == 1 || qi == 2) ? -b : b;
 }
 
-// Two Box-Muller pairs from one Philox block.
+// log((w + 0.5) 2^-32) for the Box-Muller radius: table-driven (bm_log_table.inc), division- and
+// branch-free, no special cases (the argument is always in [2^-33, 1)).  x = w + 0.5 = 2^e m, the
+// top 7 mantissa bits select c (c = 1 for the intervals next to 1, so results near 0 keep full
+// relative precision); r = m' inv_c - 1 with |r| < 2^-7; log = e ln2 + T + log1p(r), log1p by a
+// degree-8 Horner polynomial.
+static __device__ const double kBmLogTab[128][4] = {BM_LOG_TABLE_ROWS};
+
+__device__ __forceinline__ double bm_log_u32(uint32_t w) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double x = (double)w + 0.5;                                   // exact
+    const uint64_t b = d2bits(x);
+    const uint32_t top7 = (uint32_t)(b >> 45) & 0x7fu;
+    const uint32_t up = top7 >> 6;                                      // m in [1.5, 2): use m/2
+    const int e = (int)(uint32_t)(b >> 52) - 1023 + (int)up - 32;
+    const double m = bits2d((b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52));
+    typedef double f64x2_t __attribute__((ext_vector_type(2)));
+    const f64x2_t* row = reinterpret_cast<const f64x2_t*>(kBmLogTab[top7]);
+    const f64x2_t a = row[0], t = row[1];                               // (inv_c, T_hi), (T_lo, 0)
+    const double r = __builtin_fma(m, a.x, -1.0);
+    double P = __builtin_fma(r, -0x1p-3, 0x1.2492492492492p-3);         // -1/8, 1/7
+    P = __builtin_fma(r, P, -0x1.5555555555555p-3);                     // -1/6
+    P = __builtin_fma(r, P, 0x1.999999999999ap-3);                      // 1/5
+    P = __builtin_fma(r, P, -0x1p-2);                                   // -1/4
+    P = __builtin_fma(r, P, 0x1.5555555555555p-2);                      // 1/3
+    P = __builtin_fma(r, P, -0x1p-1);                                   // -1/2
+    const double p = __builtin_fma(r * r, P, r);
+    const double de = (double)e;
+    const double hi = __builtin_fma(de, ln2_hi, a.y);
+    const double lo = __builtin_fma(de, ln2_lo, t.x) + p;
+    return hi + lo;
+}
+
+// det_sincos2pi(w 2^-32) with the quarter-turn reduction done in integers: q = floor(4u + 1/2) =
+// (w + 2^29) >> 30 and u - q/4 = ((w + 2^29) mod 2^30 - 2^29) 2^-32 -- the same q and r bit for bit.
+__device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, double& c_out) {
+    const uint32_t t = w + 0x20000000u;
+    const int qi = (int)(t >> 30);
+    const double r = (double)((int32_t)(t & 0x3fffffffu) - 0x20000000) * 0x1p-32;
+    const double r2 = r * r;
+    double S = -0x1.6fadb9f155744p-1;
+    S = __builtin_fma(S, r2, 0x1.e8f434d018d63p+1);
+    S = __builtin_fma(S, r2, -0x1.e3074fde8871fp+3);
+    S = __builtin_fma(S, r2, 0x1.50783487ee782p+5);
+    S = __builtin_fma(S, r2, -0x1.32d2cce62bd86p+6);
+    S = __builtin_fma(S, r2, 0x1.466bc6775aae2p+6);
+    S = __builtin_fma(S, r2, -0x1.4abbce625be53p+5);
+    S = __builtin_fma(S, r2, 0x1.921fb54442d18p+2);
+    double C = 0x1.20c62c2f2d7f5p-2;
+    C = __builtin_fma(C, r2, -0x1.b6e24f44b128fp+0);
+    C = __builtin_fma(C, r2, 0x1.f9d38a3763cc3p+2);
+    C = __builtin_fma(C, r2, -0x1.a6d1f2a204a8cp+4);
+    C = __builtin_fma(C, r2, 0x1.e1f506891babbp+5);
+    C = __builtin_fma(C, r2, -0x1.55d3c7e3cbffap+6);
+    C = __builtin_fma(C, r2, 0x1.03c1f081b5ac4p+6);
+    C = __builtin_fma(C, r2, -0x1.3bd3cc9be45dep+4);
+    C = __builtin_fma(C, r2, 1.0);
+    const double sn = r * S;
+    const double a = (qi & 1) ? C : sn;
+    const double b = (qi & 1) ? sn : C;
+    s_out = (qi & 2) ? -a : a;
+    c_out = (qi == 1 || qi == 2) ? -b : b;
+}
+
+// Two Box-Muller pairs from one Philox block: radius sqrt(-2 log u1), u1 = (w.x + 1/2) 2^-32 in (0,1);
+// angle 2 pi u2, u2 = w.y 2^-32.
 __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3) {
     {
-        const double rad = __builtin_sqrt(-2.0 * det_log(uniform32_open(w.x)));
+        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.x));
         double s, c;
-        det_sincos2pi(uniform32(w.y), s, c);
+        det_sincos2pi_u32(w.y, s, c);
         z0 = rad * c; z1 = rad * s;
     }
     {
-        const double rad = __builtin_sqrt(-2.0 * det_log(uniform32_open(w.z)));
+        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.z));
         double s, c;
-        det_sincos2pi(uniform32(w.w), s, c);
+        det_sincos2pi_u32(w.w, s, c);
         z2 = rad * c; z3 = rad * s;
     }
 }

@@ -53,23 +53,24 @@ struct LaneChain {
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)b; }
     __device__ __forceinline__ double reduce(double v) const { return v; }
     // running addresses (see store_kept): no per-coordinate uniform offsets live across the step loop
+    // (the opaque value is the element offset, not the pointer, so the accesses stay global_*, not flat_*)
     __device__ __forceinline__ void load(const double* x, int64_t ld, double (&v)[NC]) const {
-        const double* p = x + (live ? c : 0);
+        uint64_t o = (uint64_t)(live ? c : 0);
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-            v[k] = valid(k) ? *p : 0.0;
-            p += ld;
-            asm volatile("" : "+v"(p));
+            v[k] = valid(k) ? x[o] : 0.0;
+            o += (uint64_t)ld;
+            asm volatile("" : "+v"(o));
         }
     }
     __device__ __forceinline__ void store(double* x, int64_t ld, const double (&v)[NC]) const {
         if (!live) return;
-        double* p = x + c;
+        uint64_t o = (uint64_t)c;
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-            if (valid(k)) *p = v[k];
-            p += ld;
-            asm volatile("" : "+v"(p));
+            if (valid(k)) x[o] = v[k];
+            o += (uint64_t)ld;
+            asm volatile("" : "+v"(o));
         }
     }
     __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
@@ -83,15 +84,16 @@ struct LaneChain {
     __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
                                                double* base) const {
         if (base == nullptr || !live) return;
-        double* p = base + (size_t)kk * (size_t)d * (size_t)s.C + (size_t)c;
-        const size_t C = (size_t)s.C;
+        double* p = base + (size_t)kk * (size_t)d * (size_t)s.C;
+        const uint64_t C = (uint64_t)s.C;
+        uint64_t o = (uint64_t)c;
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-            if (valid(k)) *p = v[k];
-            p += C;
-            // one running address: otherwise the NC uniform offsets k*C are precomputed and held in
+            if (valid(k)) p[o] = v[k];
+            o += C;
+            // one running offset: otherwise the NC uniform offsets k*C are precomputed and held in
             // SGPRs across the step loop, spilling the scalar file
-            asm volatile("" : "+v"(p));
+            asm volatile("" : "+v"(o));
         }
     }
     // add this chain's evaluation count to the launch-wide counter (one atomic per wave)

@@ -28,6 +28,8 @@
 #include <string.h>
 #include <math.h>
 
+#include "bm_log_table.inc"
+
 #define ORC_PHILOX_M0 0xD2511F53u
 #define ORC_PHILOX_M1 0xCD9E8D57u
 #define ORC_PHILOX_W0 0x9E3779B9u
@@ -181,14 +183,47 @@ static inline void orc_sincos2pi(double u, double* s_out, double* c_out) {
     *s_out = so; *c_out = co;
 }
 
+/* ------------------------------------------------------- Box-Muller radius logarithm */
+/* log((w + 0.5) 2^-32), w a 32-bit draw: x = w + 0.5 = 2^e m (exact); the top 7 mantissa bits pick
+   the table row (scripts/gen_bm_log_table.py): for m >= 1.5 the reduction uses m/2 and e+1, and the
+   rows next to 1 have c = 1, so a result near 0 keeps its relative precision.  r = m' inv_c - 1
+   (|r| < 2^-7), log = e ln2 + (T_hi + T_lo) + log1p(r), log1p by Horner to degree 8.  The device
+   twin is bm_log_u32 (csrc/detmath.hpp). */
+static const double orc_bm_log_tab[128][4] = {BM_LOG_TABLE_ROWS};
+
+static inline double orc_bm_log_u32(uint32_t w) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    double x = (double)w + 0.5;
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    uint32_t top7 = (uint32_t)(b >> 45) & 0x7fu;
+    uint32_t up = top7 >> 6;
+    int e = (int)(uint32_t)(b >> 52) - 1023 + (int)up - 32;
+    uint64_t mb = (b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52);
+    double m;
+    memcpy(&m, &mb, 8);
+    const double* row = orc_bm_log_tab[top7];
+    double r = fma(m, row[0], -1.0);
+    double P = fma(r, -0x1p-3, 0x1.2492492492492p-3);
+    P = fma(r, P, -0x1.5555555555555p-3);
+    P = fma(r, P, 0x1.999999999999ap-3);
+    P = fma(r, P, -0x1p-2);
+    P = fma(r, P, 0x1.5555555555555p-2);
+    P = fma(r, P, -0x1p-1);
+    double p = fma(r * r, P, r);
+    double de = (double)e;
+    double hi = fma(de, ln2_hi, row[1]);
+    double lo = fma(de, ln2_lo, row[2]) + p;
+    return hi + lo;
+}
+
 /* Four standard normals from one Philox block (two Box-Muller pairs). */
 static inline void orc_normals4(const uint32_t w[4], double z[4]) {
     for (int p = 0; p < 2; ++p) {
-        double u1 = orc_uniform32_open(w[2 * p]);
-        double u2 = orc_uniform32(w[2 * p + 1]);
-        double rad = sqrt(-2.0 * orc_log(u1));
+        double rad = sqrt(-2.0 * orc_bm_log_u32(w[2 * p]));
         double s, c;
-        orc_sincos2pi(u2, &s, &c);
+        orc_sincos2pi(orc_uniform32(w[2 * p + 1]), &s, &c);
         z[2 * p] = rad * c;
         z[2 * p + 1] = rad * s;
     }

@@ -51,7 +51,8 @@ def _dev_math(op, x, y=None):
 
 
 @pytest.mark.parametrize("op,name", [(0, "log"), (1, "exp"), (2, "sin2pi"), (3, "cos2pi"), (4, "sqrt"),
-                                     (5, "div"), (7, "round")])
+                                     (5, "div"), (7, "round"), (9, "bm_log_u32"), (10, "sin2pi_u32"),
+                                     (11, "cos2pi_u32")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -62,6 +63,10 @@ def test_device_detmath_bitwise(gpu, op, name):
         x = np.floor(rng.uniform(0, 2**32, 200000)) * 2.0**-32
     elif op == 4:
         x = np.exp(rng.uniform(-700, 700, 200000))
+    elif op in (9, 10, 11):      # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
+        x = np.concatenate([np.floor(rng.uniform(0, 2**32, 200000)), np.arange(0, 2000),
+                            2.0**32 - 1 - np.arange(0, 2000), (np.arange(-40, 40) + 2**29 * np.arange(1, 8)[:, None]
+                                                               ).ravel() % 2**32])
     elif op == 5:
         x = rng.normal(size=200000) * np.exp(rng.uniform(-300, 300, 200000))
     else:

@@ -390,3 +390,14 @@ def test_oracle_ess_matches_numpy_stats(vtype, name, phi):
     np.testing.assert_allclose(eo.T, en, rtol=1e-10)
     if phi == 0.7 and name == "imse":            # AR(1): ESS ~ n (1 - phi) / (1 + phi)
         assert abs(np.mean(eo) / (n * 0.3 / 1.7) - 1) < 0.35
+
+
+def test_bm_log_u32_accuracy():
+    """Box-Muller radius log((w + 1/2) 2^-32): <= 1 ulp against numpy's log, including near u = 1 and u -> 0."""
+    rng = np.random.default_rng(9)
+    w = np.concatenate([np.floor(rng.uniform(0, 2**32, 300000)), np.arange(0, 5000), 2.0**32 - 1 - np.arange(0, 5000),
+                        (np.arange(-64, 64) + 2.0**26 * np.arange(1, 64)[:, None]).ravel()])
+    got = orc.detmath(9, w)
+    ref = np.log((w + 0.5) * 2.0**-32)
+    err = np.abs(got - ref) / np.spacing(np.abs(ref))
+    assert err.max() <= 1.0
