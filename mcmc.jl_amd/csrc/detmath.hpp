@@ -168,7 +168,7 @@ __device__ __forceinline__ void det_sincos2pi(double u, double& s_out, double& c
 // degree-8 Horner polynomial.
 static __device__ const double kBmLogTab[128][4] = {BM_LOG_TABLE_ROWS};
 
-__device__ __forceinline__ double bm_log_u32(uint32_t w) {
+__device__ __forceinline__ double bm_log_u32(uint32_t w, const double (*tab)[4] = kBmLogTab) {
     const double ln2_hi = 0x1.62e42fee00000p-1;
     const double ln2_lo = 0x1.a39ef35793c76p-33;
     const double x = (double)w + 0.5;                                   // exact
@@ -178,7 +178,7 @@ __device__ __forceinline__ double bm_log_u32(uint32_t w) {
     const int e = (int)(uint32_t)(b >> 52) - 1023 + (int)up - 32;
     const double m = bits2d((b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52));
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    const f64x2_t* row = reinterpret_cast<const f64x2_t*>(kBmLogTab[top7]);
+    const f64x2_t* row = reinterpret_cast<const f64x2_t*>(tab[top7]);
     const f64x2_t a = row[0], t = row[1];                               // (inv_c, T_hi), (T_lo, 0)
     const double r = __builtin_fma(m, a.x, -1.0);
     double P = __builtin_fma(r, -0x1p-3, 0x1.2492492492492p-3);         // -1/8, 1/7
@@ -227,15 +227,17 @@ __device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, dou
 
 // Two Box-Muller pairs from one Philox block: radius sqrt(-2 log u1), u1 = (w.x + 1/2) 2^-32 in (0,1);
 // angle 2 pi u2, u2 = w.y 2^-32.
-__device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3) {
+// tab: the radius-log table, in global memory (default) or a kernel's LDS copy (stage_bm_log_table)
+__device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3,
+                                         const double (*tab)[4] = kBmLogTab) {
     {
-        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.x));
+        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.x, tab));
         double s, c;
         det_sincos2pi_u32(w.y, s, c);
         z0 = rad * c; z1 = rad * s;
     }
     {
-        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.z));
+        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.z, tab));
         double s, c;
         det_sincos2pi_u32(w.w, s, c);
         z2 = rad * c; z3 = rad * s;

@@ -6,9 +6,9 @@ namespace mcmc {
 
 // F: d == 4 NB (LaneChain FULL); US: uniform RWM scale
 template <int NB, bool F, class M, bool US>
-__global__ __launch_bounds__(kBlock) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
+__global__ __launch_bounds__(kBlock, 2) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
 template <int NB, bool F, class M>
-__global__ __launch_bounds__(kBlock) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
+__global__ __launch_bounds__(kBlock, 2) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
 template <int NB, bool F, class M, bool DA>
 __global__ __launch_bounds__(kBlock) void lpc_hmc(KernelArgs a) { hmc_body<LaneChain<NB, F>, M, DA>(a); }
 template <int NB, class M>

@@ -33,32 +33,65 @@ __global__ __launch_bounds__(256) void k_fma(double* out, int iters, double a0, 
     if (s == 12345.678) out[threadIdx.x] = s;
 }
 
-int main() {
-    int dev = 0, cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    double* out;
-    hipMalloc(&out, 4096);
+__global__ __launch_bounds__(256) void k_mad64(unsigned long long* out, int iters, unsigned a0) {
+    unsigned long long c[8];
+    for (int k = 0; k < 8; ++k) c[k] = threadIdx.x + k;
+    unsigned a = a0 + threadIdx.x;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = (unsigned long long)a * (unsigned)(c[k] >> 7) + (c[k] & 0xffffffffull);
+    }
+    unsigned long long s = 0;
+    for (int k = 0; k < 8; ++k) s += c[k];
+    if (s == 12345) out[threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_xor(unsigned* out, int iters, unsigned a0) {
+    unsigned c[8];
+    for (int k = 0; k < 8; ++k) c[k] = threadIdx.x * 7 + k;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = (c[k] ^ a0) + (c[k] >> 3);
+    }
+    unsigned s = 0;
+    for (int k = 0; k < 8; ++k) s += c[k];
+    if (s == 12345) out[threadIdx.x] = s;
+}
+
+static float time_it(void (*launch)(int), int iters) {
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    const int blocks = cus * 8;           // 8 blocks x 4 waves per CU: 8 waves per SIMD
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    launch(100);
+    (void)hipEventRecord(e0);
+    launch(iters);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms;
+}
+
+static double* g_out;
+static int g_blocks;
+
+int main() {
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    (void)hipMalloc(&g_out, 4096);
+    g_blocks = cus * 8;                    // 8 blocks x 4 waves per CU: 8 waves per SIMD
     const int iters = 20000;
-    float ms;
-    k_mfma<<<blocks, 256>>>(out, 100, 1.0, 1.0);
-    hipEventRecord(e0);
-    k_mfma<<<blocks, 256>>>(out, iters, 1.0000001, 0.9999999);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
-    hipEventElapsedTime(&ms, e0, e1);
-    const double mfma_flop = (double)blocks * 4 /*waves*/ * iters * 4 /*mfma*/ * 2048.0;
-    printf("{\"cus\": %d, \"mfma_f64_16x16x4_tflops\": %.2f, ", cus, mfma_flop / (ms * 1e-3) / 1e12);
-    k_fma<<<blocks, 256>>>(out, 100, 1.0, 1.0);
-    hipEventRecord(e0);
-    k_fma<<<blocks, 256>>>(out, iters, 0.9999999, 1e-9);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
-    hipEventElapsedTime(&ms, e0, e1);
-    const double fma_flop = (double)blocks * 256 * iters * 8 * 2.0;
-    printf("\"valu_fma_f64_tflops\": %.2f}\n", fma_flop / (ms * 1e-3) / 1e12);
+    const double waves = (double)g_blocks * 4;
+    const float t_mfma = time_it([](int it) { k_mfma<<<g_blocks, 256>>>(g_out, it, 1.0000001, 0.9999999); }, iters);
+    const float t_fma = time_it([](int it) { k_fma<<<g_blocks, 256>>>(g_out, it, 0.9999999, 1e-9); }, iters);
+    const float t_mad = time_it([](int it) { k_mad64<<<g_blocks, 256>>>((unsigned long long*)g_out, it, 3u); }, iters);
+    const float t_xor = time_it([](int it) { k_xor<<<g_blocks, 256>>>((unsigned*)g_out, it, 5u); }, iters);
+    // wave-instructions per second for 8 independent chains per iteration
+    const double wi = waves * iters * 8;
+    printf("{\"cus\": %d, \"mfma_f64_16x16x4_tflops\": %.2f, \"valu_fma_f64_tflops\": %.2f, "
+           "\"fma_f64_Gwave_instr_per_s\": %.1f, \"mad_u64_u32_Gwave_instr_per_s\": %.1f, "
+           "\"xad_shift_Gwave_instr_per_s\": %.1f}\n",
+           cus, waves * iters * 4 * 2048.0 / (t_mfma * 1e-3) / 1e12, waves * 64 * iters * 8 * 2.0 / (t_fma * 1e-3) / 1e12,
+           wi / (t_fma * 1e-3) / 1e9, wi / (t_mad * 1e-3) / 1e9, 2 * wi / (t_xor * 1e-3) / 1e9);
     return 0;
 }
