@@ -225,7 +225,8 @@ def main():
         torch.cuda.synchronize(dev)
         te = time.perf_counter()
         ess = mc.stats.ess_device(samples, "imse")
-        ess_min_sum = ess.min(dim=0).values.sum()
+        # a chain that never moved has a 0/0 ESS (var.jl gives NaN); it counts as 0 effective samples
+        ess_min_sum = torch.nan_to_num(ess, nan=0.0).min(dim=0).values.sum()
         torch.cuda.synchronize(dev)
         ess_s = time.perf_counter() - te
         if dist is not None:

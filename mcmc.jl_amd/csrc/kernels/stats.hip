@@ -47,9 +47,22 @@ __global__ __launch_bounds__(kEssBlock) void k_ess(EssArgs a) {
     S.stride = (size_t)a.d * (size_t)a.C;
     S.col = a.s + (size_t)j * (size_t)a.C + (size_t)(live ? c : 0);
     S.lds = stage + threadIdx.x;
-    // mean (mean.jl:6): left to right
+    // mean (mean.jl:6): left to right.  Rows are loaded 8 at a time so that 8 coalesced 512 B loads
+    // per wave are in flight (the staging pass is latency-bound otherwise: few waves fit beside the
+    // [n][64] LDS image).
     double sum = 0.0;
-    for (int64_t t = 0; t < n; ++t) {
+    int64_t t = 0;
+    for (; t + 8 <= n; t += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = S.col[(size_t)(t + u) * S.stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (LDS) stage[(size_t)(t + u) * kEssBlock + threadIdx.x] = v[u];
+            sum = sum + v[u];
+        }
+    }
+    for (; t < n; ++t) {
         const double v = S.col[(size_t)t * S.stride];
         if (LDS) stage[(size_t)t * kEssBlock + threadIdx.x] = v;
         sum = sum + v;
