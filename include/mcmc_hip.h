@@ -63,7 +63,8 @@ enum {
     MCMC_MODEL_ISO_NORMAL_DOT = 1,   /* model(v -> -dot(v,v), grad = v -> -2v)   README.md:60,63      */
     MCMC_MODEL_NORMAL_DSL = 2,       /* model(:(v ~ Normal(mu, sigma)), gradient=true)  README.md:67-72 */
     MCMC_MODEL_LOGISTIC = 3,         /* examples/logistic_regression.jl:16-22 (DSL, gradient=true)   */
-    MCMC_MODEL_LINEAR = 4            /* examples/linear_regression.jl:14-20  (DSL, gradient=true)    */
+    MCMC_MODEL_LINEAR = 4,           /* examples/linear_regression.jl:14-20  (DSL, gradient=true)    */
+    MCMC_MODEL_ABS_NORMAL_DSL = 5    /* model(:(y = abs(x); y ~ Normal(mu, sigma)))  README.md:246-251 */
 };
 
 /* samplers */
@@ -79,7 +80,7 @@ typedef struct {
     int64_t d;               /* parameter vector size (model.size)                               */
     const double* init;      /* [d]  model.init                                                  */
     const double* scale;     /* [d]  model.scale (NULL -> ones)                                   */
-    double mu, sigma;        /* NORMAL_DSL: Normal(mu, sigma)                                     */
+    double mu, sigma;        /* NORMAL_DSL, ABS_NORMAL_DSL: Normal(mu, sigma)                     */
     double prior_sigma;      /* LOGISTIC/LINEAR: vars ~ Normal(0, prior_sigma)                    */
     double noise_sigma;      /* LINEAR: resid ~ Normal(0, noise_sigma)                             */
     double link_sign;        /* LOGISTIC: +1 -> prob = 1/(1+exp(-X*vars)) (example),

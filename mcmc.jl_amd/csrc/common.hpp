@@ -4,7 +4,7 @@
 
 namespace mcmc {
 
-enum ModelKind : int32_t { MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4 };
+enum ModelKind : int32_t { MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4, MK_ABS_NORMAL = 5 };
 enum SamplerKind : int32_t { SK_RWM = 1, SK_MALA = 2, SK_HMC = 3, SK_HMCDA = 4 };
 
 // Model parameters as the kernels see them (device pointers).

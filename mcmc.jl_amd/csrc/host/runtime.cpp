@@ -307,6 +307,9 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
         case MCMC_MODEL_NORMAL_DSL:
             if (!(desc->sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "Normal sigma should be > 0"));
             break;
+        case MCMC_MODEL_ABS_NORMAL_DSL:
+            if (!(desc->sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "Normal sigma should be > 0"));
+            break;
         case MCMC_MODEL_LOGISTIC:
         case MCMC_MODEL_LINEAR: {
             if (d > mcmc_glm_max_d()) return bail(fail(MCMC_E_UNSUPPORTED, "regression models support d <= 512"));
@@ -377,7 +380,7 @@ extern "C" int mcmc_model_destroy(mcmc_model* m) {
 }
 
 static bool model_is_separable(const mcmc_model* m) {
-    return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL;
+    return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL || m->args.kind == MK_ABS_NORMAL;
 }
 static bool model_is_glm(const mcmc_model* m) { return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR; }
 

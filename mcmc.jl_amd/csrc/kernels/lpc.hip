@@ -37,6 +37,7 @@ template <int NB, bool F>
 static hipError_t launch_nbf(const KernelArgs& a, hipStream_t st) {
     if (a.m.kind == MK_ISO) return launch_model<NB, F, IsoDot>(a, st);
     if (a.m.kind == MK_NORMAL) return launch_model<NB, F, NormalDSL>(a, st);
+    if (a.m.kind == MK_ABS_NORMAL) return launch_model<NB, F, AbsNormalDSL>(a, st);
     return hipErrorInvalidValue;
 }
 
@@ -51,6 +52,7 @@ static hipError_t launch_eval_nb(const KernelArgs& a, const double* xin, double*
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
     if (a.m.kind == MK_ISO) lpc_eval<NB, IsoDot><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else if (a.m.kind == MK_NORMAL) lpc_eval<NB, NormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
+    else if (a.m.kind == MK_ABS_NORMAL) lpc_eval<NB, AbsNormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -35,6 +35,7 @@ template <int NB>
 static hipError_t launch_nb(const KernelArgs& a, hipStream_t st) {
     if (a.m.kind == MK_ISO) return launch_model<NB, IsoDot>(a, st);
     if (a.m.kind == MK_NORMAL) return launch_model<NB, NormalDSL>(a, st);
+    if (a.m.kind == MK_ABS_NORMAL) return launch_model<NB, AbsNormalDSL>(a, st);
     return hipErrorInvalidValue;
 }
 
@@ -44,6 +45,7 @@ static hipError_t launch_eval_nb(const KernelArgs& a, const double* xin, double*
     const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
     if (a.m.kind == MK_ISO) wpc_eval<NB, IsoDot><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else if (a.m.kind == MK_NORMAL) wpc_eval<NB, NormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
+    else if (a.m.kind == MK_ABS_NORMAL) wpc_eval<NB, AbsNormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

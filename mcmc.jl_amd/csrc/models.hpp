@@ -13,6 +13,10 @@
 //              generated function turns into (-Inf, zero(beta))
 //              (AccumulatorDerivRules.jl:14-16, modelparser.jl:64-72).
 //              Gradient rule dx += (mu - x)/(sigma*sigma) * ds (MCMCDerivRules.jl:57).
+//   AbsNormalDSL :(y = abs(x); y ~ Normal(mu, sigma))   README.md:246-251 (the SeqMC example):
+//              lp = LLAcc(0.) + sum(logpdf(Normal(mu,sigma), |v|)).  Gradient: the Normal rule
+//              times d|v|/dv = sign(v) (ReverseDiffSource's rule for abs is not vendored: that
+//              factor is "parity unpinned"; the README example runs RWM, which needs no gradient).
 //
 // Summation: the reference sums with BLAS ddot / Julia `sum`; the build fixes
 // the order so that the oracle can restate it exactly: lane-per-chain kernels
@@ -50,6 +54,24 @@ struct NormalDSL {
     }
     __device__ __forceinline__ double finish(double a) const { return a; }
     __device__ __forceinline__ double grad(double v) const { return (mu - v) / s2; }
+};
+
+struct AbsNormalDSL {
+    static constexpr bool kLLAcc = true;
+    double mu, sigma, logsig, s2;
+    __device__ explicit AbsNormalDSL(const ModelArgs& m) : mu(m.mu), sigma(m.sigma) {
+        logsig = det_log(sigma);
+        s2 = sigma * sigma;
+    }
+    __device__ __forceinline__ void acc(double& a, double v) const {
+        const double z = (__builtin_fabs(v) - mu) / sigma;
+        a = a + (-0.5 * (z * z + kLog2Pi) - logsig);
+    }
+    __device__ __forceinline__ double finish(double a) const { return a; }
+    __device__ __forceinline__ double grad(double v) const {
+        const double sg = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0);
+        return sg * ((mu - __builtin_fabs(v)) / s2);
+    }
 };
 
 // LLAcc rule: a non-finite total means out of support -> (-Inf, 0).

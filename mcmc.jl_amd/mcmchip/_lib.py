@@ -25,6 +25,7 @@ MODEL_ISO_NORMAL_DOT = 1
 MODEL_NORMAL_DSL = 2
 MODEL_LOGISTIC = 3
 MODEL_LINEAR = 4
+MODEL_ABS_NORMAL_DSL = 5
 
 SAMPLER_RWM = 1
 SAMPLER_MALA = 2

@@ -30,7 +30,7 @@ from . import _lib
 from ._lib import check, dptr
 
 __all__ = [
-    "IsoNormalDot", "NormalDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
+    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
     "RWM", "MALA", "HMC", "HMCDA", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
     "run", "resume", "device_count",
 ]
@@ -70,6 +70,14 @@ class IsoNormalDot:
 class NormalDSL:
     """The DSL model `v ~ Normal(mu, sigma)` with gradient=true (README.md:67-72)."""
     kind = _lib.MODEL_NORMAL_DSL
+
+    def __init__(self, mu: float = 0.0, sigma: float = 1.0):
+        self.mu, self.sigma = float(mu), float(sigma)
+
+
+class AbsNormalDSL:
+    """The DSL model `y = abs(x); y ~ Normal(mu, sigma)` (README.md:246-251, the SeqMC example)."""
+    kind = _lib.MODEL_ABS_NORMAL_DSL
 
     def __init__(self, mu: float = 0.0, sigma: float = 1.0):
         self.mu, self.sigma = float(mu), float(sigma)

@@ -29,6 +29,7 @@
 #define ORC_MODEL_NORMAL 2
 #define ORC_MODEL_LOGISTIC 3
 #define ORC_MODEL_LINEAR 4
+#define ORC_MODEL_ABS_NORMAL 5
 
 #define ORC_RWM 1
 #define ORC_MALA 2
@@ -273,12 +274,14 @@ static double orc_eval(const orc_model* m, const double* x, double* g, double* t
             for (int j = 0; j < d; ++j) g[j] = -2.0 * x[j];
         return lp;
     }
-    if (m->kind == ORC_MODEL_NORMAL) {
+    if (m->kind == ORC_MODEL_NORMAL || m->kind == ORC_MODEL_ABS_NORMAL) {
         /* v ~ Normal(mu, sigma): LLAcc(0.) + sum(logpdf(...)) (AccumulatorDerivRules.jl:10-20,
-           modelparser.jl:48-51); gradient rule dx += (mu - x)/(sigma*sigma)*ds (MCMCDerivRules.jl:57) */
+           modelparser.jl:48-51); gradient rule dx += (mu - x)/(sigma*sigma)*ds (MCMCDerivRules.jl:57).
+           ABS_NORMAL: y = abs(x); y ~ Normal(mu, sigma) (README.md:246-251), gradient times sign(x). */
+        const int ab = m->kind == ORC_MODEL_ABS_NORMAL;
         const double logsig = orc_log(m->sigma);
         for (int j = 0; j < d; ++j) {
-            double z = (x[j] - m->mu) / m->sigma;
+            double z = ((ab ? fabs(x[j]) : x[j]) - m->mu) / m->sigma;
             tmp[j] = -0.5 * (z * z + ORC_LOG2PI) - logsig;
         }
         double lp = orc_sum(tmp, m, order);
@@ -286,7 +289,14 @@ static double orc_eval(const orc_model* m, const double* x, double* g, double* t
         if (oos) lp = -INFINITY;                  /* OutOfSupportError -> (-Inf, zero(beta)), modelparser.jl:64-72 */
         if (g) {
             const double s2 = m->sigma * m->sigma;
-            for (int j = 0; j < d; ++j) g[j] = oos ? 0.0 : (m->mu - x[j]) / s2;
+            for (int j = 0; j < d; ++j) {
+                if (ab) {
+                    const double sg = x[j] > 0.0 ? 1.0 : (x[j] < 0.0 ? -1.0 : 0.0);
+                    g[j] = oos ? 0.0 : sg * ((m->mu - fabs(x[j])) / s2);
+                } else {
+                    g[j] = oos ? 0.0 : (m->mu - x[j]) / s2;
+                }
+            }
         }
         return lp;
     }

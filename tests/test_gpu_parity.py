@@ -91,6 +91,8 @@ def _model(kind, d):
     if kind == "iso":
         return mc.model(mc.IsoNormalDot(), init=np.linspace(0.5, 1.5, d), grad=True,
                         scale=np.linspace(0.8, 1.2, d))
+    if kind == "abs":
+        return mc.model(mc.AbsNormalDSL(1.0, 0.7), x=np.linspace(-1, 1, d), gradient=True)
     return mc.model(mc.NormalDSL(0.3, 1.7), v=np.linspace(-1, 1, d), gradient=True)
 
 
@@ -121,7 +123,7 @@ def order_for(d):
 
 
 @pytest.mark.parametrize("sname", list(SAMPLERS))
-@pytest.mark.parametrize("mkind", ["iso", "normal"])
+@pytest.mark.parametrize("mkind", ["iso", "normal", "abs"])
 @pytest.mark.parametrize("d", [1, 3, 7, 16, 32, 33, 100, 256, 257, 1024])
 def test_sampler_parity(gpu, sname, mkind, d):
     m = _model(mkind, d)

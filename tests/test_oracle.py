@@ -401,3 +401,19 @@ def test_bm_log_u32_accuracy():
     ref = np.log((w + 0.5) * 2.0**-32)
     err = np.abs(got - ref) / np.spacing(np.abs(ref))
     assert err.max() <= 1.0
+
+
+def test_abs_normal_dsl_closed_form_and_gradient():
+    """y = abs(x); y ~ Normal(mu, sigma) (README.md:246-251): lp = sum logpdf(Normal, |x|), grad = sign(x) (mu-|x|)/s^2."""
+    mu, sig = 1.0, 0.7
+    m = mc.model(mc.AbsNormalDSL(mu, sig), x=np.zeros(5), gradient=True)
+    x = np.array([[-1.3, 0.2, 2.0, -0.4, 1.1], [0.5, -0.5, 3.0, 1.0, -2.2]]).T
+    lp, g = orc.eval_batch(m, x)
+    ref = stats.norm.logpdf(np.abs(x), mu, sig).sum(axis=0)
+    np.testing.assert_allclose(lp, ref, rtol=1e-13)
+    np.testing.assert_allclose(g, np.sign(x) * (mu - np.abs(x)) / sig**2, rtol=1e-13)
+    h = 1e-6
+    for j in range(5):
+        e = np.zeros((5, 1)); e[j] = h
+        fd = (orc.eval_batch(m, x[:, :1] + e)[0] - orc.eval_batch(m, x[:, :1] - e)[0]) / (2 * h)
+        assert abs(fd[0] - g[j, 0]) < 1e-6
