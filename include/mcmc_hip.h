@@ -174,6 +174,29 @@ int mcmc_chains_set_store_gradients(mcmc_chains* chains, int32_t store);
 /* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
 int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);
 
+/* ---- SeqMC population runner (src/runners/SeqMC.jl:21-122) ----
+ * targets[t] (t < ntargets) are chain batches of one context, equal d, each with nchains == npart:
+ * particle n is chain n of every target.  Per outer step i = 1..steps and target t: every particle is
+ * reset into target t (state = particle, lp = eval: MCMC.reset, MCMC.jl:39) and advanced one step of
+ * its sampler; logW += lp_t(reset) - logtarget; logtarget = lp after the step; when var(exp(logW)) <
+ * trigger the particles are resampled multinomially from cumsum(W)/sum(W) (one Philox uniform of
+ * (particle, i, t, tag 2) under `seed`) and logW = 0.  After each outer step logtarget = 0, and for
+ * i > burnin the particles and exp(logW) are stored.
+ *   particles : [d][npart] start values (SeqMC.jl:43 `particles`)
+ *   samples   : [steps-burnin][d][npart]   (row i-burnin-1: the particles after outer step i)
+ *   weights   : [steps-burnin][npart]      (diagnostics["weigths"])
+ *   resampled : [steps][ntargets] int32 flags, or NULL
+ * on_device != 0: particles/samples/weights/resampled are device pointers on the context's GPU. */
+typedef struct {
+    int64_t steps;           /* SeqMC.steps   (SeqMC.jl:24)                                          */
+    int64_t burnin;          /* SeqMC.burnin                                                          */
+    double trigger;          /* SeqMC.trigger: resample when var(W) < trigger                        */
+} mcmc_seqmc_cfg;
+int mcmc_seqmc_validate(const mcmc_seqmc_cfg* cfg);
+int mcmc_run_seqmc(mcmc_chains* const* targets, int32_t ntargets, int64_t npart, const double* particles,
+                   const mcmc_seqmc_cfg* cfg, uint64_t seed, int32_t on_device, double* samples, double* weights,
+                   int32_t* resampled, double* runtime_s);
+
 /* ---- output analysis (src/stats/ess.jl:6-10, var.jl:7-117) ----
  * Effective sample size n * var_iid / var_vtype of every (parameter j, chain c) series of
  * samples [nkept][d][nchains] (the mcmc_outputs layout).  vtype: MCMC_VAR_IMSE (Geyer initial

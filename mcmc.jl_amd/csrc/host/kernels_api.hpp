@@ -29,6 +29,15 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_glm_max_d();
+// SeqMC population bookkeeping (seqmc.hip)
+hipError_t mcmc_seqmc_weights(int64_t N, double* logW, const double* ll0, double* logtarget, const double* plogtarget,
+                              hipStream_t st);
+hipError_t mcmc_seqmc_scan(int64_t N, const double* logW, double trigger, double* cp, int32_t* flag, hipStream_t st);
+hipError_t mcmc_seqmc_resample(int64_t N, int d, const double* cp, const int32_t* flag, uint64_t seed, uint32_t step,
+                               uint32_t target, const double* pars, double* pars_out, const double* logtarget,
+                               double* logtarget_out, double* logW, hipStream_t st);
+hipError_t mcmc_seqmc_store(int64_t N, int d, const double* pars, const double* logW, double* samples, double* weights,
+                            hipStream_t st);
 // effective sample size of every (parameter, chain) series of samples [n][d][C] (stats.hip)
 hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t C, int32_t vtype, int64_t maxlag,
                            int64_t batchlen, double* ess, double* var, hipStream_t st);

@@ -791,6 +791,144 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
 }
 
 // ------------------------------------------------------------------ debug probes
+// ------------------------------------------------------------------ SeqMC (SeqMC.jl:21-122)
+extern "C" int mcmc_seqmc_validate(const mcmc_seqmc_cfg* cfg) {
+    if (!cfg) return fail(MCMC_E_INVALID_ARG, "seqmc cfg is NULL");
+    char buf[160];
+    if (!(cfg->burnin >= 0)) {
+        snprintf(buf, sizeof buf, "Burnin rounds (%lld) should be >= 0", (long long)cfg->burnin);        // SeqMC.jl:30
+        return fail(MCMC_E_INVALID_ARG, buf);
+    }
+    if (!(cfg->steps > cfg->burnin)) {
+        snprintf(buf, sizeof buf, "Steps (%lld) should be > to burnin (%lld)", (long long)cfg->steps,
+                 (long long)cfg->burnin);                                                                 // SeqMC.jl:31
+        return fail(MCMC_E_INVALID_ARG, buf);
+    }
+    return MCMC_OK;
+}
+
+// One sampler step of every chain of `c` from its current state, nothing kept (the SamplerTask's
+// `consume` inside run_seqmc, SeqMC.jl:69).
+static int step_once(mcmc_chains* c, hipStream_t st) {
+    mcmc_model* m = c->model;
+    KernelArgs a = base_args(m, c->C, c->ld);
+    a.sa = c->sa;
+    a.st = c->st;
+    StepArgs& s = a.s;
+    s.chain0 = (uint32_t)c->offset;
+    s.key0 = (uint32_t)c->seed;
+    s.key1 = (uint32_t)(c->seed >> 32);
+    s.run_step0 = c->steps_done;
+    s.burnin = 0;
+    s.thinning = 1;
+    s.len = 1;
+    s.tuner_burnin = 0;
+    s.scale = c->d_scale_eff;
+    s.scale1 = c->scale1;
+    s.scale_uniform = c->scale_uniform;
+    s.samples = nullptr;
+    s.grads = nullptr;
+    s.acc_bits = nullptr;
+    s.nw = (c->C + 63) / 64;
+    s.n_evals = c->d_evals;
+    s.step_begin = c->steps_done + 1;
+    s.nsteps = 1;
+    HIP_TRY(launch_step(c->layout, a, st));
+    c->steps_done += 1;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_run_seqmc(mcmc_chains* const* targets, int32_t ntargets, int64_t npart, const double* particles,
+                              const mcmc_seqmc_cfg* cfg, uint64_t seed, int32_t on_device, double* samples,
+                              double* weights, int32_t* resampled, double* runtime_s) {
+    if (!targets || ntargets < 1 || !particles || !cfg) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    if (int r = mcmc_seqmc_validate(cfg)) return r;
+    if (npart < 1) return fail(MCMC_E_INVALID_ARG, "need at least one particle");
+    for (int t = 0; t < ntargets; ++t)
+        if (!targets[t]) return fail(MCMC_E_INVALID_ARG, "NULL target");
+    mcmc_ctx* ctx = targets[0]->model->ctx;
+    const int d = targets[0]->model->args.d;
+    for (int t = 0; t < ntargets; ++t) {
+        if (targets[t]->model->args.d != d)
+            return fail(MCMC_E_INVALID_ARG, "Models do not have the same parameter vector size");  // SeqMC.jl:49
+        if (targets[t]->model->ctx != ctx) return fail(MCMC_E_INVALID_ARG, "targets live on different contexts");
+        if (targets[t]->C != npart) return fail(MCMC_E_INVALID_ARG, "every target needs nchains == npart");
+    }
+    if (cfg->steps > 0xffffffffLL) return fail(MCMC_E_INVALID_ARG, "steps exceed 2^32");
+    if (int r = set_device(ctx)) return r;
+    hipStream_t st = ctx->stream;
+    const size_t nd = (size_t)d * (size_t)npart, N = (size_t)npart;
+    const int64_t nstore = cfg->steps - cfg->burnin;
+    double *parsA = nullptr, *parsB = nullptr, *logW = nullptr, *lt = nullptr, *lt2 = nullptr, *ll0 = nullptr,
+           *cp = nullptr, *dsamp = nullptr, *dw = nullptr;
+    int32_t *flags = nullptr;
+    int rc = MCMC_OK;
+    auto t0 = std::chrono::steady_clock::now();
+    do {
+        if ((rc = dmalloc(&parsA, nd)) || (rc = dmalloc(&parsB, nd)) || (rc = dmalloc(&logW, N)) ||
+            (rc = dmalloc(&lt, N)) || (rc = dmalloc(&lt2, N)) || (rc = dmalloc(&ll0, N)) || (rc = dmalloc(&cp, N)) ||
+            (rc = dmalloc(&flags, (size_t)cfg->steps * ntargets)))
+            break;
+        if (on_device) {
+            dsamp = samples;
+            dw = weights;
+        } else if ((samples && (rc = dmalloc(&dsamp, (size_t)nstore * nd))) ||
+                   (weights && (rc = dmalloc(&dw, (size_t)nstore * N)))) {
+            break;
+        }
+        hipError_t e = on_device ? hipMemcpyAsync(parsA, particles, nd * 8, hipMemcpyDeviceToDevice, st)
+                                 : h2d(ctx, parsA, particles, nd * 8);
+        if (e == hipSuccess) e = dzero(ctx, logW, N * 8);                       // logW = zeros(npart)
+        if (e == hipSuccess) e = dzero(ctx, lt, N * 8);                         // logtarget = zeros(npart)
+        for (int64_t i = 1; e == hipSuccess && i <= cfg->steps; ++i) {
+            for (int t = 0; e == hipSuccess && t < ntargets; ++t) {
+                mcmc_chains* c = targets[t];
+                KernelArgs a = base_args(c->model, c->C, c->ld);
+                // MCMC.reset(t, pars[n]): state <- particle, logtarget <- eval (RWM.jl:49, MALA.jl:75-78)
+                e = cols_to_state(c->layout, c->st.x, c->ld, parsA, npart, d, npart, st);
+                if (e == hipSuccess) e = launch_eval(c->layout, a, c->st.x, c->st.lp, c->st.g, 0, st);
+                if (e == hipSuccess) e = hipMemcpyAsync(ll0, c->st.lp, N * 8, hipMemcpyDeviceToDevice, st);
+                if (e != hipSuccess) break;
+                if ((rc = step_once(c, st))) break;                             // sample = consume(t.task)
+                e = state_to_cols(c->layout, parsA, npart, c->st.x, c->ld, d, npart, st);   // pars[n] = ppars
+                if (e == hipSuccess) e = mcmc_seqmc_weights(npart, logW, ll0, lt, c->st.lp, st);
+                int32_t* flag = flags + (size_t)(i - 1) * ntargets + t;
+                if (e == hipSuccess) e = mcmc_seqmc_scan(npart, logW, cfg->trigger, cp, flag, st);
+                if (e == hipSuccess)
+                    e = mcmc_seqmc_resample(npart, d, cp, flag, seed, (uint32_t)i, (uint32_t)t, parsA, parsB, lt, lt2,
+                                            logW, st);
+                std::swap(parsA, parsB);
+                std::swap(lt, lt2);
+            }
+            if (rc) break;
+            if (e == hipSuccess) e = dzero(ctx, lt, N * 8);                     // logtarget = zeros(npart)
+            if (e == hipSuccess && i > cfg->burnin && (dsamp || dw)) {
+                const size_t row = (size_t)(i - cfg->burnin - 1);
+                double* ps = dsamp ? dsamp + row * nd : parsB;                  // parsB: scratch when not wanted
+                double* pw = dw ? dw + row * N : ll0;
+                e = mcmc_seqmc_store(npart, d, parsA, logW, ps, pw, st);
+            }
+        }
+        if (rc) break;
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess && !on_device) {
+            if (samples) e = d2h(ctx, samples, dsamp, (size_t)nstore * nd * 8);
+            if (e == hipSuccess && weights) e = d2h(ctx, weights, dw, (size_t)nstore * N * 8);
+        }
+        if (e == hipSuccess && resampled) {
+            e = on_device ? hipMemcpyAsync(resampled, flags, (size_t)cfg->steps * ntargets * 4, hipMemcpyDeviceToDevice, st)
+                          : d2h(ctx, resampled, flags, (size_t)cfg->steps * ntargets * 4);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+        }
+        if (e != hipSuccess) rc = fail(MCMC_E_HIP, std::string("seqmc: ") + hipGetErrorString(e));
+    } while (0);
+    (void)hipStreamSynchronize(st);
+    if (runtime_s) *runtime_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    dfree(parsA); dfree(parsB); dfree(logW); dfree(lt); dfree(lt2); dfree(ll0); dfree(cp); dfree(flags);
+    if (!on_device) { dfree(dsamp); dfree(dw); }
+    return rc;
+}
+
 extern "C" int mcmc_stats_ess(mcmc_ctx* ctx, const double* samples, int64_t nkept, int64_t d, int64_t nchains,
                               int32_t vtype, int64_t maxlag, int64_t batchlen, int32_t on_device, double* ess,
                               double* var) {

@@ -9,6 +9,8 @@ from .api import (  # noqa: F401
     RWM, MALA, HMC, HMCDA, EmpMCTuner, EmpiricalMCMCTuner, SerialMC, MCMCTask, MCMCChain,
     run, resume, device_count,
 )
+from .seqmc import SeqMC, SeqMCChain, run_seqmc, resume_seqmc  # noqa: F401
+from . import stats  # noqa: F401
 from .stats import acceptance, mean, var, ess, actime, mcvar_iid, mcvar_bm, mcvar_imse, mcvar_ipse  # noqa: F401
 
 MCMCLikModel = MCMCLikelihoodModel

@@ -403,8 +403,8 @@ class MCMCTask:
     def __init__(self, model: MCMCLikelihoodModel, sampler: _Sampler, runner: SerialMC, nchains: int = 1,
                  seed: int = 1, device: int = 0, chain_offset: int = 0, init_x=None, steps_per_launch: int = 0):
         self._h = None
-        if not isinstance(runner, SerialMC):
-            raise NotImplementedError("only the SerialMC runner drives the batched kernels")
+        if not isinstance(runner, SerialMC) and type(runner).__name__ != "SeqMC":
+            raise NotImplementedError("runners: SerialMC (one batch) or SeqMC (lists of targets, run_seqmc)")
         if sampler.kind != _lib.SAMPLER_RWM and not model.has_gradient:
             name = type(sampler).__name__
             raise AssertionError(f"{name} sampler requires model with gradient function")
@@ -542,6 +542,9 @@ def run(t, *args, nchains: Optional[int] = None, seed: Optional[int] = None, **k
         kinds = {type(x.runner if isinstance(x, MCMCTask) else x.task.runner) for x in t}
         if len(kinds) != 1:
             raise AssertionError("Runners do not have the same runner type")
+        if next(iter(kinds)).__name__ == "SeqMC":                 # run(t::Array{MCMCTask}) -> run_seqmc
+            from .seqmc import run_seqmc
+            return run_seqmc(t, seed=1 if seed is None else seed, **kw)
         return [run(x, nchains=nchains, seed=seed, **kw) for x in t]
     if isinstance(t, MCMCChain):                              # run(c::MCMCChain) = run(c.task)
         return _run_task(t.task)

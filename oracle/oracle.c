@@ -692,3 +692,117 @@ void orc_ess(const double* samples, int64_t n, int64_t d, int64_t C, int vtype, 
                              var ? var + o : NULL);
     }
 }
+
+/* ------------------------------------------------------------ SeqMC population runner
+ * run_seqmc (SeqMC.jl:43-122): particle n is chain n of every target.  Per outer step i and target t:
+ * reset (state <- particle, lp <- eval; MCMC.reset, RWM.jl:49), one sampler step, logW += lp(reset) -
+ * logtarget, logtarget <- lp after the step; resample multinomially when var(exp(logW)) < trigger.
+ * The weight reductions follow kernels/seqmc.hip exactly: 256 chunks of ceil(N/256) particles summed
+ * left to right, the chunk sums added left to right; cp[n] = (exclusive chunk prefix + running chunk
+ * sum) / total; the resampling uniform is Philox (particle n, i, t, tag 2) under `seed`. */
+#define ORC_SEQ_T 256
+#define ORC_TAG_RESAMPLE 2u
+
+void orc_seqmc(const orc_model* const* models, const orc_sampler* const* samplers, const uint64_t* seeds,
+               orc_state* const* states, int64_t* steps_done, int ntargets, int64_t N, const double* particles,
+               int64_t steps, int64_t burnin, double trigger, uint64_t seed, int order, double* samples,
+               double* weights, int32_t* resampled) {
+    const int d = models[0]->d;
+    size_t sc = 0;
+    for (int t = 0; t < ntargets; ++t) {
+        size_t s1 = orc_scratch(models[t]);
+        if (s1 > sc) sc = s1;
+    }
+    double* pars = (double*)malloc(sizeof(double) * (size_t)d * N);
+    double* pars2 = (double*)malloc(sizeof(double) * (size_t)d * N);
+    double* logW = (double*)calloc((size_t)N, sizeof(double));
+    double* lt = (double*)calloc((size_t)N, sizeof(double));
+    double* lt2 = (double*)malloc(sizeof(double) * N);
+    double* ll0 = (double*)malloc(sizeof(double) * N);
+    double* cp = (double*)malloc(sizeof(double) * N);
+    double* xv = (double*)malloc(sizeof(double) * ((size_t)d + sc));
+    double* tmp = xv + d;
+    memcpy(pars, particles, sizeof(double) * (size_t)d * N);
+    const int64_t chunk = (N + ORC_SEQ_T - 1) / ORC_SEQ_T;
+    for (int64_t i = 1; i <= steps; ++i) {
+        for (int t = 0; t < ntargets; ++t) {
+            const orc_model* m = models[t];
+            orc_state* st = states[t];
+            for (int64_t n = 0; n < N; ++n) {                       /* MCMC.reset(t, pars[n]) */
+                for (int j = 0; j < d; ++j) {
+                    st->x[(size_t)j * N + n] = pars[(size_t)j * N + n];
+                    xv[j] = pars[(size_t)j * N + n];
+                }
+                st->lp[n] = orc_eval(m, xv, NULL, tmp, order);
+                ll0[n] = st->lp[n];
+            }
+            orc_run(m, samplers[t], seeds[t], 0, N, 0, N, steps_done[t], 0, 1, 1, st, NULL, NULL, NULL, order, 1);
+            steps_done[t] += 1;
+            memcpy(pars, st->x, sizeof(double) * (size_t)d * N);      /* pars[n] = sample.ppars */
+            for (int64_t n = 0; n < N; ++n) {
+                logW[n] = logW[n] + (ll0[n] - lt[n]);
+                lt[n] = st->lp[n];
+            }
+            /* var(W) and cumsum(W)/sum(W) in the kernel's chunked order */
+            double part[ORC_SEQ_T], qpart[ORC_SEQ_T];
+            for (int k = 0; k < ORC_SEQ_T; ++k) {
+                int64_t b = (int64_t)k * chunk, e = b + chunk < N ? b + chunk : N;
+                double s = 0.0;
+                for (int64_t n = b; n < e; ++n) s = s + orc_exp(logW[n]);
+                part[k] = s;
+            }
+            double total = 0.0;
+            for (int k = 0; k < ORC_SEQ_T; ++k) total = total + part[k];
+            const double mean = total / (double)N;
+            for (int k = 0; k < ORC_SEQ_T; ++k) {
+                int64_t b = (int64_t)k * chunk, e = b + chunk < N ? b + chunk : N;
+                double q = 0.0;
+                for (int64_t n = b; n < e; ++n) {
+                    double dv = orc_exp(logW[n]) - mean;
+                    q = q + dv * dv;
+                }
+                qpart[k] = q;
+            }
+            double ss = 0.0;
+            for (int k = 0; k < ORC_SEQ_T; ++k) ss = ss + qpart[k];
+            const int flag = (ss / (double)(N - 1)) < trigger;
+            if (resampled) resampled[(size_t)(i - 1) * ntargets + t] = flag;
+            double run = 0.0;
+            for (int k = 0; k < ORC_SEQ_T; ++k) {
+                int64_t b = (int64_t)k * chunk, e = b + chunk < N ? b + chunk : N;
+                double pre = run;
+                for (int64_t n = b; n < e; ++n) {
+                    pre = pre + orc_exp(logW[n]);
+                    cp[n] = pre / total;
+                }
+                run = run + part[k];
+            }
+            if (flag) {
+                for (int64_t n = 0; n < N; ++n) {
+                    uint32_t w[4];
+                    orc_block(seed, (uint32_t)n, (uint32_t)i, (uint32_t)t, ORC_TAG_RESAMPLE, w);
+                    const double u = orc_uniform53(w[0], w[1]);
+                    int64_t lo = 0, hi = N - 1;
+                    while (lo < hi) {
+                        int64_t mid = lo + (hi - lo) / 2;
+                        if (cp[mid] >= u) hi = mid;
+                        else lo = mid + 1;
+                    }
+                    for (int j = 0; j < d; ++j) pars2[(size_t)j * N + n] = pars[(size_t)j * N + lo];
+                    lt2[n] = lt[lo];
+                }
+                for (int64_t n = 0; n < N; ++n) logW[n] = 0.0;
+                memcpy(pars, pars2, sizeof(double) * (size_t)d * N);
+                memcpy(lt, lt2, sizeof(double) * N);
+            }
+        }
+        for (int64_t n = 0; n < N; ++n) lt[n] = 0.0;                 /* logtarget = zeros(npart) */
+        if (i > burnin) {
+            const size_t row = (size_t)(i - burnin - 1);
+            if (samples) memcpy(samples + row * (size_t)d * N, pars, sizeof(double) * (size_t)d * N);
+            if (weights)
+                for (int64_t n = 0; n < N; ++n) weights[row * N + n] = orc_exp(logW[n]);
+        }
+    }
+    free(pars); free(pars2); free(logW); free(lt); free(lt2); free(ll0); free(cp); free(xv);
+}

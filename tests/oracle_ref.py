@@ -160,6 +160,34 @@ class OracleChains:
         return samples, grads, acc
 
 
+def seqmc(targets, particles, steps, burnin, trigger, seed, target_seeds, order=0):
+    """orc_seqmc: run_seqmc (SeqMC.jl:43-122) over [(model, sampler), ...] with particles [npart, d].
+    Returns samples [steps-burnin][d][npart], weights [steps-burnin][npart], resampled flags [steps][nt]."""
+    P = np.asarray(particles, dtype=np.float64)
+    npart, d = P.shape
+    chains = [OracleChains(m, s, nchains=npart, seed=ts, order=order) for (m, s), ts in zip(targets, target_seeds)]
+    nt = len(chains)
+    models = (ct.POINTER(OModel) * nt)(*[ct.pointer(c.om.s) for c in chains])
+    samplers = (ct.POINTER(OSampler) * nt)(*[ct.pointer(c.os) for c in chains])
+    states = (ct.POINTER(OState) * nt)(*[ct.pointer(c.st) for c in chains])
+    seeds = (ct.c_uint64 * nt)(*[c.seed for c in chains])
+    done = (ct.c_int64 * nt)(*([0] * nt))
+    nst = steps - burnin
+    samples = np.empty((nst, d, npart))
+    weights = np.empty((nst, npart))
+    flags = np.zeros((steps, nt), dtype=np.int32)
+    part = np.ascontiguousarray(P.T)
+    L = lib()
+    L.orc_seqmc.restype = None
+    L.orc_seqmc.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_int, ct.c_int64, D,
+                            ct.c_int64, ct.c_int64, ct.c_double, ct.c_uint64, ct.c_int, D, D,
+                            ct.POINTER(ct.c_int32)]
+    L.orc_seqmc(models, samplers, seeds, states, done, nt, npart, _d(part), steps, burnin, trigger,
+                ct.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), order, _d(samples), _d(weights),
+                flags.ctypes.data_as(ct.POINTER(ct.c_int32)))
+    return samples, weights, flags
+
+
 def eval_batch(m, xs, order=0):
     om = OracleModel(m)
     xs = np.ascontiguousarray(np.asarray(xs, dtype=np.float64).reshape(m.size, -1))
