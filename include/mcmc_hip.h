@@ -64,7 +64,23 @@ enum {
     MCMC_MODEL_NORMAL_DSL = 2,       /* model(:(v ~ Normal(mu, sigma)), gradient=true)  README.md:67-72 */
     MCMC_MODEL_LOGISTIC = 3,         /* examples/logistic_regression.jl:16-22 (DSL, gradient=true)   */
     MCMC_MODEL_LINEAR = 4,           /* examples/linear_regression.jl:14-20  (DSL, gradient=true)    */
-    MCMC_MODEL_ABS_NORMAL_DSL = 5    /* model(:(y = abs(x); y ~ Normal(mu, sigma)))  README.md:246-251 */
+    MCMC_MODEL_ABS_NORMAL_DSL = 5,   /* model(:(y = abs(x); y ~ Normal(mu, sigma)))  README.md:246-251 */
+    MCMC_MODEL_DIST_DSL = 6          /* model(:(v ~ Dist(p1, p2))): dist = MCMC_DIST_*, p1 = mu, p2 = sigma */
+};
+
+/* distributions of MCMC_MODEL_DIST_DSL: the DSL's continuous logpdf rules, MCMCDerivRules.jl:56-104
+   (Distributions.jl parametrisations) */
+enum {
+    MCMC_DIST_NORMAL = 1,       /* Normal(mu, sigma)          */
+    MCMC_DIST_UNIFORM = 2,      /* Uniform(a, b)              */
+    MCMC_DIST_WEIBULL = 3,      /* Weibull(shape, scale)      */
+    MCMC_DIST_BETA = 4,         /* Beta(alpha, beta)          */
+    MCMC_DIST_TDIST = 5,        /* TDist(df)     (p2 unused)  */
+    MCMC_DIST_EXPONENTIAL = 6,  /* Exponential(scale)         */
+    MCMC_DIST_GAMMA = 7,        /* Gamma(shape, scale)        */
+    MCMC_DIST_CAUCHY = 8,       /* Cauchy(location, scale)    */
+    MCMC_DIST_LOGNORMAL = 9,    /* LogNormal(meanlog, sdlog)  */
+    MCMC_DIST_LAPLACE = 10      /* Laplace(location, scale)   */
 };
 
 /* samplers */
@@ -88,6 +104,7 @@ typedef struct {
     int64_t n;               /* observations                                                      */
     const double* X;         /* [n][d] row-major covariates                                        */
     const double* Y;         /* [n] responses (LOGISTIC: 0.0 / 1.0)                                */
+    int32_t dist;            /* DIST_DSL: MCMC_DIST_* (parameters in mu, sigma)                     */
 } mcmc_model_desc;
 
 typedef struct {

@@ -4,14 +4,21 @@
 
 namespace mcmc {
 
-enum ModelKind : int32_t { MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4, MK_ABS_NORMAL = 5 };
+enum ModelKind : int32_t { MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4, MK_ABS_NORMAL = 5, MK_DIST = 6 };
+// MK_DIST: v ~ Dist(p1, p2) elementwise (MCMCDerivRules.jl:56-104, the DSL's continuous distributions)
+enum DistKind : int32_t {
+    DK_NORMAL = 1, DK_UNIFORM = 2, DK_WEIBULL = 3, DK_BETA = 4, DK_TDIST = 5, DK_EXPONENTIAL = 6, DK_GAMMA = 7,
+    DK_CAUCHY = 8, DK_LOGNORMAL = 9, DK_LAPLACE = 10
+};
 enum SamplerKind : int32_t { SK_RWM = 1, SK_MALA = 2, SK_HMC = 3, SK_HMCDA = 4 };
 
 // Model parameters as the kernels see them (device pointers).
 struct ModelArgs {
     int32_t kind;
     int32_t d;
-    double mu, sigma;           // NORMAL_DSL
+    double mu, sigma;           // NORMAL_DSL, ABS_NORMAL_DSL; DIST: the two parameters p1, p2
+    int32_t dist;               // DIST: DistKind
+    double dconst;              // DIST: host-computed constant of the logpdf (lgamma terms etc.)
     double prior_sigma;         // regression prior
     double noise_sigma;         // LINEAR
     double link_sign;           // LOGISTIC

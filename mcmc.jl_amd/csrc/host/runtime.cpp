@@ -310,6 +310,32 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
         case MCMC_MODEL_ABS_NORMAL_DSL:
             if (!(desc->sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "Normal sigma should be > 0"));
             break;
+        case MCMC_MODEL_DIST_DSL: {
+            const double p1 = desc->mu, p2 = desc->sigma;
+            const double kPi = 3.14159265358979323846;
+            double c = 0.0;
+            bool ok = true;
+            switch (desc->dist) {
+                case MCMC_DIST_NORMAL: ok = p2 > 0; c = -std::log(p2); break;
+                case MCMC_DIST_UNIFORM: ok = p1 < p2; c = -std::log(p2 - p1); break;
+                case MCMC_DIST_WEIBULL: ok = p1 > 0 && p2 > 0; c = std::log(p1 / p2); break;
+                case MCMC_DIST_BETA: ok = p1 > 0 && p2 > 0; c = std::lgamma(p1 + p2) - std::lgamma(p1) - std::lgamma(p2); break;
+                case MCMC_DIST_TDIST:
+                    ok = p1 > 0;
+                    c = std::lgamma((p1 + 1.0) / 2.0) - std::lgamma(p1 / 2.0) - 0.5 * std::log(p1 * kPi);
+                    break;
+                case MCMC_DIST_EXPONENTIAL: ok = p1 > 0; c = -std::log(p1); break;
+                case MCMC_DIST_GAMMA: ok = p1 > 0 && p2 > 0; c = -std::lgamma(p1) - p1 * std::log(p2); break;
+                case MCMC_DIST_CAUCHY: ok = p2 > 0; c = -std::log(kPi * p2); break;
+                case MCMC_DIST_LOGNORMAL: ok = p2 > 0; c = -std::log(p2) - 0.5 * std::log(2.0 * kPi); break;
+                case MCMC_DIST_LAPLACE: ok = p2 > 0; c = -std::log(2.0 * p2); break;
+                default: return bail(fail(MCMC_E_UNSUPPORTED, "unknown distribution"));
+            }
+            if (!ok) return bail(fail(MCMC_E_INVALID_ARG, "invalid distribution parameters"));
+            a.dist = desc->dist;
+            a.dconst = c;
+            break;
+        }
         case MCMC_MODEL_LOGISTIC:
         case MCMC_MODEL_LINEAR: {
             if (d > mcmc_glm_max_d()) return bail(fail(MCMC_E_UNSUPPORTED, "regression models support d <= 512"));
@@ -380,7 +406,8 @@ extern "C" int mcmc_model_destroy(mcmc_model* m) {
 }
 
 static bool model_is_separable(const mcmc_model* m) {
-    return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL || m->args.kind == MK_ABS_NORMAL;
+    return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL || m->args.kind == MK_ABS_NORMAL ||
+           m->args.kind == MK_DIST;
 }
 static bool model_is_glm(const mcmc_model* m) { return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR; }
 

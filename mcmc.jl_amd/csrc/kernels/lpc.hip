@@ -38,6 +38,7 @@ static hipError_t launch_nbf(const KernelArgs& a, hipStream_t st) {
     if (a.m.kind == MK_ISO) return launch_model<NB, F, IsoDot>(a, st);
     if (a.m.kind == MK_NORMAL) return launch_model<NB, F, NormalDSL>(a, st);
     if (a.m.kind == MK_ABS_NORMAL) return launch_model<NB, F, AbsNormalDSL>(a, st);
+    if (a.m.kind == MK_DIST) return launch_model<NB, F, DistDSL>(a, st);
     return hipErrorInvalidValue;
 }
 
@@ -53,6 +54,7 @@ static hipError_t launch_eval_nb(const KernelArgs& a, const double* xin, double*
     if (a.m.kind == MK_ISO) lpc_eval<NB, IsoDot><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else if (a.m.kind == MK_NORMAL) lpc_eval<NB, NormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else if (a.m.kind == MK_ABS_NORMAL) lpc_eval<NB, AbsNormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
+    else if (a.m.kind == MK_DIST) lpc_eval<NB, DistDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -36,6 +36,7 @@ static hipError_t launch_nb(const KernelArgs& a, hipStream_t st) {
     if (a.m.kind == MK_ISO) return launch_model<NB, IsoDot>(a, st);
     if (a.m.kind == MK_NORMAL) return launch_model<NB, NormalDSL>(a, st);
     if (a.m.kind == MK_ABS_NORMAL) return launch_model<NB, AbsNormalDSL>(a, st);
+    if (a.m.kind == MK_DIST) return launch_model<NB, DistDSL>(a, st);
     return hipErrorInvalidValue;
 }
 
@@ -46,6 +47,7 @@ static hipError_t launch_eval_nb(const KernelArgs& a, const double* xin, double*
     if (a.m.kind == MK_ISO) wpc_eval<NB, IsoDot><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else if (a.m.kind == MK_NORMAL) wpc_eval<NB, NormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else if (a.m.kind == MK_ABS_NORMAL) wpc_eval<NB, AbsNormalDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
+    else if (a.m.kind == MK_DIST) wpc_eval<NB, DistDSL><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

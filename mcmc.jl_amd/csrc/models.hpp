@@ -74,6 +74,64 @@ struct AbsNormalDSL {
     }
 };
 
+// v ~ Dist(p1, p2) elementwise: logpdf and the x-derivative rules of MCMCDerivRules.jl:56-104
+// (Distributions.jl parametrisations: Weibull(shape, scale), Beta(alpha, beta), TDist(df),
+// Exponential(scale), Gamma(shape, scale), Cauchy(location, scale), LogNormal(meanlog, sdlog),
+// Laplace(location, scale), Uniform(a, b)).  Outside the support the term is -Inf, which the LLAcc rule
+// turns into (-Inf, zero gradient).  `c` holds the parameter-only part (lgamma / log terms), computed on
+// the host (restated by oracle/oracle.c orc_dist_const).  The distribution is uniform over a launch:
+// the switch is a scalar branch.
+struct DistDSL {
+    static constexpr bool kLLAcc = true;
+    int32_t dist;
+    double p1, p2, c;
+    __device__ explicit DistDSL(const ModelArgs& m) : dist(m.dist), p1(m.mu), p2(m.sigma), c(m.dconst) {
+    }
+    __device__ __forceinline__ double logpdf(double v) const {
+        const double ninf = -__builtin_inf();
+        switch (dist) {
+            case DK_NORMAL: { const double z = (v - p1) / p2; return -0.5 * (z * z + kLog2Pi) + c; }
+            case DK_UNIFORM: return (v >= p1 && v <= p2) ? c : ninf;
+            case DK_WEIBULL: {
+                if (v < 0.0) return ninf;
+                const double lr = det_log(v / p2);
+                return c + (p1 - 1.0) * lr - det_exp(p1 * lr);
+            }
+            case DK_BETA:
+                if (v < 0.0 || v > 1.0) return ninf;
+                return (p1 - 1.0) * det_log(v) + (p2 - 1.0) * det_log(1.0 - v) + c;
+            case DK_TDIST: return c - ((p1 + 1.0) / 2.0) * det_log(1.0 + (v * v) / p1);
+            case DK_EXPONENTIAL: return v < 0.0 ? ninf : c - v / p1;
+            case DK_GAMMA: return v < 0.0 ? ninf : (p1 - 1.0) * det_log(v) - v / p2 + c;
+            case DK_CAUCHY: { const double z = (v - p1) / p2; return c - det_log(1.0 + z * z); }
+            case DK_LOGNORMAL: {
+                if (v <= 0.0) return ninf;
+                const double lv = det_log(v), e = lv - p1;
+                return -(e * e) / (2.0 * p2 * p2) - lv + c;
+            }
+            case DK_LAPLACE: return c - __builtin_fabs(v - p1) / p2;
+            default: return bits2d(0x7ff8000000000000ull);
+        }
+    }
+    __device__ __forceinline__ void acc(double& a, double v) const { a = a + logpdf(v); }
+    __device__ __forceinline__ double finish(double a) const { return a; }
+    __device__ __forceinline__ double grad(double v) const {
+        switch (dist) {
+            case DK_NORMAL: return (p1 - v) / (p2 * p2);                                       // :57
+            case DK_UNIFORM: return 0.0;                                                       // :62
+            case DK_WEIBULL: return ((1.0 - det_exp(p1 * det_log(v / p2))) * p1 - 1.0) / v;   // :69
+            case DK_BETA: return (p1 - 1.0) / v - (p2 - 1.0) / (1.0 - v);                      // :74
+            case DK_TDIST: return -(p1 + 1.0) * v / (p1 + v * v);                              // :79
+            case DK_EXPONENTIAL: return -1.0 / p1;                                             // :83
+            case DK_GAMMA: return -(p2 + v - p1 * p2) / (p2 * v);                              // :88
+            case DK_CAUCHY: { const double e = v - p1; return 2.0 * (p1 - v) / (p2 * p2 + e * e); }   // :93
+            case DK_LOGNORMAL: return (p1 - p2 * p2 - det_log(v)) / (p2 * p2 * v);             // :98
+            case DK_LAPLACE: return (v > p1 ? -1.0 : 1.0) / p2;                                // :103
+            default: return 0.0;
+        }
+    }
+};
+
 // LLAcc rule: a non-finite total means out of support -> (-Inf, 0).
 template <class M>
 __device__ __forceinline__ double llacc_finish(const M& m, double a, bool& oos) {

@@ -26,6 +26,11 @@ MODEL_NORMAL_DSL = 2
 MODEL_LOGISTIC = 3
 MODEL_LINEAR = 4
 MODEL_ABS_NORMAL_DSL = 5
+MODEL_DIST_DSL = 6
+
+# MCMC_DIST_* (include/mcmc_hip.h)
+DISTS = {"Normal": 1, "Uniform": 2, "Weibull": 3, "Beta": 4, "TDist": 5, "Exponential": 6, "Gamma": 7,
+         "Cauchy": 8, "LogNormal": 9, "Laplace": 10}
 
 SAMPLER_RWM = 1
 SAMPLER_MALA = 2
@@ -54,6 +59,7 @@ class ModelDesc(ct.Structure):
         ("mu", ct.c_double), ("sigma", ct.c_double),
         ("prior_sigma", ct.c_double), ("noise_sigma", ct.c_double), ("link_sign", ct.c_double),
         ("n", ct.c_int64), ("X", ct.POINTER(ct.c_double)), ("Y", ct.POINTER(ct.c_double)),
+        ("dist", ct.c_int32),
     ]
 
 

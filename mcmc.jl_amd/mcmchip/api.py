@@ -30,7 +30,7 @@ from . import _lib
 from ._lib import check, dptr
 
 __all__ = [
-    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
+    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
     "RWM", "MALA", "HMC", "HMCDA", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
     "run", "resume", "device_count",
 ]
@@ -81,6 +81,28 @@ class AbsNormalDSL:
 
     def __init__(self, mu: float = 0.0, sigma: float = 1.0):
         self.mu, self.sigma = float(mu), float(sigma)
+
+
+class DistDSL:
+    """The DSL statement `v ~ Dist(p1, p2)` over the parameter vector (elementwise, summed), for the DSL's
+    continuous distributions with x-derivative rules (MCMCDerivRules.jl:56-104): Normal, Uniform,
+    Weibull, Beta, TDist, Exponential, Gamma, Cauchy, LogNormal, Laplace (Distributions.jl parameters and
+    defaults)."""
+    kind = _lib.MODEL_DIST_DSL
+    _DEFAULTS = {"Normal": (0.0, 1.0), "Uniform": (0.0, 1.0), "Weibull": (1.0, 1.0), "Beta": (1.0, 1.0),
+                 "TDist": (1.0, 0.0), "Exponential": (1.0, 0.0), "Gamma": (1.0, 1.0), "Cauchy": (0.0, 1.0),
+                 "LogNormal": (0.0, 1.0), "Laplace": (0.0, 1.0)}
+
+    def __init__(self, dist: str, *params: float):
+        if dist not in _lib.DISTS:
+            raise ValueError(f"unsupported distribution {dist!r}; one of {sorted(_lib.DISTS)}")
+        p = list(self._DEFAULTS[dist])
+        if len(params) > 2:
+            raise ValueError("at most two parameters")
+        for i, v in enumerate(params):
+            p[i] = float(v)
+        self.name, self.dist = dist, _lib.DISTS[dist]
+        self.mu, self.sigma = p                         # p1, p2 in the C ABI's mu / sigma slots
 
 
 class LogisticRegression:
@@ -144,6 +166,7 @@ class MCMCLikelihoodModel:
         desc.prior_sigma = getattr(t, "prior_sigma", 1.0)
         desc.noise_sigma = getattr(t, "noise_sigma", 1.0)
         desc.link_sign = getattr(t, "link_sign", 1.0)
+        desc.dist = getattr(t, "dist", 0)
         if hasattr(t, "X"):
             desc.n = t.X.shape[0]
             desc.X = dptr(t.X)

@@ -30,6 +30,7 @@
 #define ORC_MODEL_LOGISTIC 3
 #define ORC_MODEL_LINEAR 4
 #define ORC_MODEL_ABS_NORMAL 5
+#define ORC_MODEL_DIST 6
 
 #define ORC_RWM 1
 #define ORC_MALA 2
@@ -45,6 +46,7 @@ typedef struct {
     const double* X;      /* [n][d] */
     const double* Y;      /* [n]    */
     const double* scale;  /* [d] model.scale */
+    int32_t dist;         /* ORC_MODEL_DIST: distribution (MCMC_DIST_* of include/mcmc_hip.h) */
 } orc_model;
 
 typedef struct {
@@ -264,8 +266,80 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
 
 /* ------------------------------------------------------------ models */
 /* Returns lp; writes the gradient into g (length d) when g != NULL; tmp: scratch (see orc_scratch). */
+/* v ~ Dist(p1, p2) elementwise (MCMCDerivRules.jl:56-104; Distributions.jl parametrisations).  The
+   parameter-only constant is computed as the runtime does (glibc log / lgamma), the rest as
+   csrc/models.hpp DistDSL. */
+static double orc_dist_const(int dist, double p1, double p2) {
+    const double kPi = 3.14159265358979323846;
+    switch (dist) {
+        case 1: return -log(p2);
+        case 2: return -log(p2 - p1);
+        case 3: return log(p1 / p2);
+        case 4: return lgamma(p1 + p2) - lgamma(p1) - lgamma(p2);
+        case 5: return lgamma((p1 + 1.0) / 2.0) - lgamma(p1 / 2.0) - 0.5 * log(p1 * kPi);
+        case 6: return -log(p1);
+        case 7: return -lgamma(p1) - p1 * log(p2);
+        case 8: return -log(kPi * p2);
+        case 9: return -log(p2) - 0.5 * log(2.0 * kPi);
+        case 10: return -log(2.0 * p2);
+        default: return NAN;
+    }
+}
+
+static double orc_dist_logpdf(int dist, double p1, double p2, double c, double v) {
+    switch (dist) {
+        case 1: { double z = (v - p1) / p2; return -0.5 * (z * z + ORC_LOG2PI) + c; }
+        case 2: return (v >= p1 && v <= p2) ? c : -INFINITY;
+        case 3: {
+            if (v < 0.0) return -INFINITY;
+            double lr = orc_log(v / p2);
+            return c + (p1 - 1.0) * lr - orc_exp(p1 * lr);
+        }
+        case 4:
+            if (v < 0.0 || v > 1.0) return -INFINITY;
+            return (p1 - 1.0) * orc_log(v) + (p2 - 1.0) * orc_log(1.0 - v) + c;
+        case 5: return c - ((p1 + 1.0) / 2.0) * orc_log(1.0 + (v * v) / p1);
+        case 6: return v < 0.0 ? -INFINITY : c - v / p1;
+        case 7: return v < 0.0 ? -INFINITY : (p1 - 1.0) * orc_log(v) - v / p2 + c;
+        case 8: { double z = (v - p1) / p2; return c - orc_log(1.0 + z * z); }
+        case 9: {
+            if (v <= 0.0) return -INFINITY;
+            double lv = orc_log(v), e = lv - p1;
+            return -(e * e) / (2.0 * p2 * p2) - lv + c;
+        }
+        case 10: return c - fabs(v - p1) / p2;
+        default: return NAN;
+    }
+}
+
+static double orc_dist_grad(int dist, double p1, double p2, double v) {
+    switch (dist) {
+        case 1: return (p1 - v) / (p2 * p2);
+        case 2: return 0.0;
+        case 3: return ((1.0 - orc_exp(p1 * orc_log(v / p2))) * p1 - 1.0) / v;
+        case 4: return (p1 - 1.0) / v - (p2 - 1.0) / (1.0 - v);
+        case 5: return -(p1 + 1.0) * v / (p1 + v * v);
+        case 6: return -1.0 / p1;
+        case 7: return -(p2 + v - p1 * p2) / (p2 * v);
+        case 8: { double e = v - p1; return 2.0 * (p1 - v) / (p2 * p2 + e * e); }
+        case 9: return (p1 - p2 * p2 - orc_log(v)) / (p2 * p2 * v);
+        case 10: return (v > p1 ? -1.0 : 1.0) / p2;
+        default: return 0.0;
+    }
+}
+
 static double orc_eval(const orc_model* m, const double* x, double* g, double* tmp, int order) {
     const int d = m->d;
+    if (m->kind == ORC_MODEL_DIST) {
+        const double c = orc_dist_const(m->dist, m->mu, m->sigma);
+        for (int j = 0; j < d; ++j) tmp[j] = orc_dist_logpdf(m->dist, m->mu, m->sigma, c, x[j]);
+        double lp = orc_sum(tmp, m, order);
+        int oos = !isfinite(lp);
+        if (oos) lp = -INFINITY;                  /* LLAcc: (-Inf, zero(beta)), modelparser.jl:64-72 */
+        if (g)
+            for (int j = 0; j < d; ++j) g[j] = oos ? 0.0 : orc_dist_grad(m->dist, m->mu, m->sigma, x[j]);
+        return lp;
+    }
     if (m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR) return orc_glm_eval(m, x, g, tmp);
     if (m->kind == ORC_MODEL_ISO) {
         /* model(v -> -dot(v,v), grad = v -> -2v)  README.md:60,63; test/test_syntax.jl:40-41 */

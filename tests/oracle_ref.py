@@ -23,7 +23,7 @@ D = ct.POINTER(ct.c_double)
 class OModel(ct.Structure):
     _fields_ = [("kind", ct.c_int32), ("d", ct.c_int32), ("mu", ct.c_double), ("sigma", ct.c_double),
                 ("prior_sigma", ct.c_double), ("noise_sigma", ct.c_double), ("link_sign", ct.c_double),
-                ("n", ct.c_int64), ("X", D), ("Y", D), ("scale", D)]
+                ("n", ct.c_int64), ("X", D), ("Y", D), ("scale", D), ("dist", ct.c_int32)]
 
 
 class OSampler(ct.Structure):
@@ -95,6 +95,7 @@ class OracleModel:
         s.prior_sigma = getattr(t, "prior_sigma", 1.0)
         s.noise_sigma = getattr(t, "noise_sigma", 1.0)
         s.link_sign = getattr(t, "link_sign", 1.0)
+        s.dist = getattr(t, "dist", 0)
         if self.X is not None:
             s.n = self.X.shape[0]
             s.X = _d(self.X)

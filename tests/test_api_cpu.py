@@ -37,7 +37,7 @@ def test_library_exports_every_header_symbol():
 def test_struct_layouts_match_header():
     # sizes of the C structs (LP64): checked against a compiled probe of the header
     assert ct.sizeof(_lib.RunnerCfg) == 24
-    assert ct.sizeof(_lib.ModelDesc) == 4 + 4 + 8 + 8 + 8 + 5 * 8 + 8 + 8 + 8
+    assert ct.sizeof(_lib.ModelDesc) == 4 + 4 + 8 + 8 + 8 + 5 * 8 + 8 + 8 + 8 + 8   # dist: int32 + pad
     assert ct.sizeof(_lib.SamplerCfg) == 4 + 4 + 8 + 8 + 8 + 8 + 5 * 8 + 4 + 4 + 8 + 8 + 8 + 8 + 8
     assert ct.sizeof(_lib.Outputs) == 5 * 8 + 8 + 8 + 8 + 8
 

@@ -417,3 +417,41 @@ def test_abs_normal_dsl_closed_form_and_gradient():
         e = np.zeros((5, 1)); e[j] = h
         fd = (orc.eval_batch(m, x[:, :1] + e)[0] - orc.eval_batch(m, x[:, :1] - e)[0]) / (2 * h)
         assert abs(fd[0] - g[j, 0]) < 1e-6
+
+
+DIST_CASES = [
+    ("Normal", (0.3, 1.7), lambda p: stats.norm(p[0], p[1]), (-2.0, 2.0)),
+    ("Uniform", (-1.0, 2.0), lambda p: stats.uniform(p[0], p[1] - p[0]), (-0.9, 1.9)),
+    ("Weibull", (1.5, 2.0), lambda p: stats.weibull_min(p[0], scale=p[1]), (0.1, 4.0)),
+    ("Beta", (2.0, 3.0), lambda p: stats.beta(p[0], p[1]), (0.05, 0.95)),
+    ("TDist", (3.0,), lambda p: stats.t(p[0]), (-3.0, 3.0)),
+    ("Exponential", (1.5,), lambda p: stats.expon(scale=p[0]), (0.1, 4.0)),
+    ("Gamma", (2.5, 0.7), lambda p: stats.gamma(p[0], scale=p[1]), (0.1, 4.0)),
+    ("Cauchy", (0.5, 1.3), lambda p: stats.cauchy(p[0], p[1]), (-3.0, 3.0)),
+    ("LogNormal", (0.2, 0.6), lambda p: stats.lognorm(p[1], scale=np.exp(p[0])), (0.1, 4.0)),
+    ("Laplace", (0.4, 0.9), lambda p: stats.laplace(p[0], p[1]), (-2.0, 2.0)),
+]
+
+
+@pytest.mark.parametrize("name,params,ref,rng_", DIST_CASES, ids=[c[0] for c in DIST_CASES])
+def test_dist_dsl_logpdf_gradient_and_support(name, params, ref, rng_):
+    """v ~ Dist(p1, p2) (MCMCDerivRules.jl:56-104): logpdf vs scipy, the x-derivative rule vs finite
+    differences, and -Inf with zero gradient outside the support (LLAcc)."""
+    d = 6
+    m = mc.model(mc.DistDSL(name, *params), v=np.full(d, 0.5 if name == "Beta" else 1.0), gradient=True)
+    x = np.random.default_rng(7).uniform(*rng_, size=(d, 9))
+    lp, g = orc.eval_batch(m, x)
+    np.testing.assert_allclose(lp, ref(params).logpdf(x).sum(axis=0), rtol=1e-12, atol=1e-12)
+    h = 1e-6
+    for j in range(d):
+        e = np.zeros((d, 1))
+        e[j] = h
+        fd = (orc.eval_batch(m, x[:, :1] + e)[0] - orc.eval_batch(m, x[:, :1] - e)[0]) / (2 * h)
+        if name != "Uniform":
+            assert abs(fd[0] - g[j, 0]) < 1e-5 * max(1.0, abs(g[j, 0]))
+    lo = {"Uniform": -1.5, "Weibull": -0.5, "Beta": 1.5, "Exponential": -0.1, "Gamma": -1.0, "LogNormal": -0.1}
+    if name in lo:
+        xo = x[:, :1].copy()
+        xo[2] = lo[name]
+        lpo, go = orc.eval_batch(m, xo)
+        assert lpo[0] == -np.inf and np.all(go == 0.0)
