@@ -1,0 +1,89 @@
+// lpc_impl.hpp -- lane-per-chain kernels (d <= 32): one thread = one chain; see samplers.hpp for the
+// step code and its reference lines.  Included by one translation unit per model (lpc_<model>.hip)
+// so that the instantiations compile in parallel; lpc.hip dispatches on the model kind.
+#pragma once
+#include "../samplers.hpp"
+#include "layout_api.hpp"
+
+namespace mcmc {
+
+// F: d == 4 NB (LaneChain FULL); US: uniform RWM scale
+template <int NB, bool F, class M, bool US>
+__global__ __launch_bounds__(kBlock, 2) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
+template <int NB, bool F, class M>
+__global__ __launch_bounds__(kBlock, 2) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
+template <int NB, bool F, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void lpc_hmc(KernelArgs a) { hmc_body<LaneChain<NB, F>, M, DA>(a); }
+template <int NB, class M>
+__global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
+                                                   int32_t check) {
+    eval_body<LaneChain<NB>, M>(a, xin, lp, g, check);
+}
+
+template <int NB, bool F, class M>
+static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    switch (a.sa.kind) {
+        case SK_RWM:
+            if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            break;
+        case SK_MALA: lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMC: lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMCDA: lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// SPEC: instantiate the FULL (d == 4 NB) variants too -- for the models the benchmarks run
+template <int NB, class M, bool SPEC>
+static hipError_t lpc_launch_nb(const KernelArgs& a, hipStream_t st) {
+    if (SPEC && a.s.d == 4 * NB) return lpc_launch_model<NB, SPEC, M>(a, st);
+    return lpc_launch_model<NB, false, M>(a, st);
+}
+
+template <class M, bool SPEC>
+static hipError_t lpc_step(const KernelArgs& a, hipStream_t st) {
+    switch ((a.s.d + 3) / 4) {
+        case 1: return lpc_launch_nb<1, M, SPEC>(a, st);
+        case 2: return lpc_launch_nb<2, M, SPEC>(a, st);
+        case 3: return lpc_launch_nb<3, M, SPEC>(a, st);
+        case 4: return lpc_launch_nb<4, M, SPEC>(a, st);
+        case 5: return lpc_launch_nb<5, M, SPEC>(a, st);
+        case 6: return lpc_launch_nb<6, M, SPEC>(a, st);
+        case 7: return lpc_launch_nb<7, M, SPEC>(a, st);
+        case 8: return lpc_launch_nb<8, M, SPEC>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class M>
+static hipError_t lpc_eval_m(const KernelArgs& a, const double* xin, double* lp, double* g, int check,
+                             hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    switch ((a.s.d + 3) / 4) {
+        case 1: lpc_eval<1, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 2: lpc_eval<2, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 3: lpc_eval<3, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 4: lpc_eval<4, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 5: lpc_eval<5, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 6: lpc_eval<6, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 7: lpc_eval<7, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 8: lpc_eval<8, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mcmc
+
+// one translation unit per model: LPC_UNIT(iso, IsoDot, true) defines mcmc_lpc_step_iso / mcmc_lpc_eval_iso
+#define LPC_UNIT(name, Model, SPEC)                                                                      \
+    hipError_t mcmc_lpc_step_##name(const mcmc::KernelArgs& a, hipStream_t st) {                         \
+        return mcmc::lpc_step<mcmc::Model, SPEC>(a, st);                                                \
+    }                                                                                                    \
+    hipError_t mcmc_lpc_eval_##name(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, \
+                                    int check, hipStream_t st) {                                         \
+        return mcmc::lpc_eval_m<mcmc::Model>(a, xin, lp, g, check, st);                                 \
+    }

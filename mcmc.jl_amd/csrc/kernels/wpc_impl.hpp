@@ -1,0 +1,80 @@
+// wpc_impl.hpp -- wave-per-chain kernels (32 < d <= 2048): one wave = one chain (4 chains per 256-thread
+// block); see samplers.hpp for the step code and its reference lines.  Included by one translation
+// unit per model (wpc_<model>.hip); wpc.hip dispatches on the model kind.
+#pragma once
+#include "../samplers.hpp"
+#include "layout_api.hpp"
+
+namespace mcmc {
+
+constexpr int kChainsPerBlock = kBlock / 64;
+
+template <int NB, class M>
+__global__ __launch_bounds__(kBlock) void wpc_rwm(KernelArgs a) { rwm_body<WaveChain<NB>, M>(a); }
+template <int NB, class M>
+__global__ __launch_bounds__(kBlock) void wpc_mala(KernelArgs a) { mala_body<WaveChain<NB>, M>(a); }
+template <int NB, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void wpc_hmc(KernelArgs a) { hmc_body<WaveChain<NB>, M, DA>(a); }
+template <int NB, class M>
+__global__ __launch_bounds__(kBlock) void wpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
+                                                   int32_t check) {
+    eval_body<WaveChain<NB>, M>(a, xin, lp, g, check);
+}
+
+template <int NB, class M>
+static hipError_t wpc_launch_model(const KernelArgs& a, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    switch (a.sa.kind) {
+        case SK_RWM: wpc_rwm<NB, M><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_MALA: wpc_mala<NB, M><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMC: wpc_hmc<NB, M, false><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMCDA: wpc_hmc<NB, M, true><<<grid, kBlock, 0, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// G = Philox blocks per lane: d <= 256 G, 4 (l + 64k) + e < d
+static inline int wpc_nb_for(int d) {
+    if (d <= 256) return 1;
+    if (d <= 512) return 2;
+    if (d <= 1024) return 4;
+    if (d <= 2048) return 8;
+    return 0;
+}
+
+template <class M>
+static hipError_t wpc_step(const KernelArgs& a, hipStream_t st) {
+    switch (wpc_nb_for(a.s.d)) {
+        case 1: return wpc_launch_model<1, M>(a, st);
+        case 2: return wpc_launch_model<2, M>(a, st);
+        case 4: return wpc_launch_model<4, M>(a, st);
+        case 8: return wpc_launch_model<8, M>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class M>
+static hipError_t wpc_eval_m(const KernelArgs& a, const double* xin, double* lp, double* g, int check,
+                             hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    switch (wpc_nb_for(a.s.d)) {
+        case 1: wpc_eval<1, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 2: wpc_eval<2, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 4: wpc_eval<4, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 8: wpc_eval<8, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mcmc
+
+#define WPC_UNIT(name, Model)                                                                            \
+    hipError_t mcmc_wpc_step_##name(const mcmc::KernelArgs& a, hipStream_t st) {                         \
+        return mcmc::wpc_step<mcmc::Model>(a, st);                                                      \
+    }                                                                                                    \
+    hipError_t mcmc_wpc_eval_##name(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, \
+                                    int check, hipStream_t st) {                                         \
+        return mcmc::wpc_eval_m<mcmc::Model>(a, xin, lp, g, check, st);                                 \
+    }

@@ -10,6 +10,6 @@ step() {
   echo "$name exit $rc" | tee -a "$O/steps.txt"
   case $rc in 0|1|2|5) return 0;; *) echo "fatal rc $rc in $name: stopping"; exit $rc;; esac
 }
-step r1r_seq 600 python3 -m pytest tests/test_seqmc.py -q -m gpu
+step r1r_seq 600 python3 -m pytest tests/test_gpu_parity.py -q -m gpu -k dist_dsl
 step r1r_gpu 900 python3 -m pytest tests -q -m gpu
 echo all-done
