@@ -8,6 +8,7 @@ struct ModelDesc                   # mcmc_model_desc
     init::Ptr{Float64}; scale::Ptr{Float64}
     mu::Float64; sigma::Float64; prior_sigma::Float64; noise_sigma::Float64; link_sign::Float64
     n::Int64; X::Ptr{Float64}; Y::Ptr{Float64}
+    dist::Int32                    # MODEL_DIST_DSL: MCMC_DIST_*, parameters in mu / sigma
 end
 struct SamplerCfg                  # mcmc_sampler_cfg
     kind::Int32; scale::Float64; drift_step::Float64; n_leaps::Int64; leap_step::Float64
@@ -23,6 +24,7 @@ mutable struct Outputs             # mcmc_outputs (mutable: the library writes r
 end
 
 const MODEL_ISO_NORMAL_DOT, MODEL_NORMAL_DSL, MODEL_LOGISTIC, MODEL_LINEAR = 1, 2, 3, 4
+const MODEL_ABS_NORMAL_DSL, MODEL_DIST_DSL = 5, 6
 const RWM_K, MALA_K, HMC_K, HMCDA_K = 1, 2, 3, 4
 
 check(st) = st == 0 ? nothing :
@@ -37,7 +39,7 @@ end
 # model(v -> -dot(v,v), grad = v -> -2v, init = ...)   (README.md:60-63)
 function isonormal_model(ctx, init::Vector{Float64}; scale = ones(length(init)))
     desc = ModelDesc(MODEL_ISO_NORMAL_DOT, 1, length(init), pointer(init), pointer(scale),
-                     0.0, 1.0, 1.0, 1.0, 1.0, 0, C_NULL, C_NULL)
+                     0.0, 1.0, 1.0, 1.0, 1.0, 0, C_NULL, C_NULL, 0)
     h = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve init scale check(ccall((:mcmc_model_create, lib), Cint,
         (Ptr{Cvoid}, Ref{ModelDesc}, Ptr{Ptr{Cvoid}}), ctx, desc, h))
@@ -48,7 +50,7 @@ end
 function logistic_model(ctx, X::Matrix{Float64}, Y::Vector{Float64}; init = zeros(size(X, 2)))
     Xr = collect(transpose(X)); scale = ones(size(X, 2))
     desc = ModelDesc(MODEL_LOGISTIC, 1, size(X, 2), pointer(init), pointer(scale),
-                     0.0, 1.0, 1.0, 1.0, 1.0, size(X, 1), pointer(Xr), pointer(Y))
+                     0.0, 1.0, 1.0, 1.0, 1.0, size(X, 1), pointer(Xr), pointer(Y), 0)
     h = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve Xr Y init scale check(ccall((:mcmc_model_create, lib), Cint,
         (Ptr{Cvoid}, Ref{ModelDesc}, Ptr{Ptr{Cvoid}}), ctx, desc, h))
