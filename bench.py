@@ -52,6 +52,12 @@ CONFIGS = {
     "linear512": dict(model="linear", d=512, n=4096, chains=65536 // 8, sampler="hmcda", steps=20, warmup=2,
                       thinning=1, desc="config 5: linear regression n=4096 d=512, HMCDA(), 65,536 chains over 8 "
                                        "GPUs (8,192/GPU); 20 steps: each step is ~len/eps leapfrogs"),
+    # the adaptive RAM sampler (not a BASELINE config)
+    "ram32": dict(model="iso", d=32, chains=1 << 18, sampler="ram", steps=200, warmup=20, thinning=10,
+                  desc="RAM(1., 0.234) on d=32 iso-Normal, 262,144 chains (a 32x32 jump factor per chain)"),
+    "ramlinear": dict(model="linear", d=10, n=1000, chains=1 << 16, sampler="ram", steps=200, warmup=20,
+                      thinning=10, desc="examples/linear_regression.jl:28: RAM(1., 0.3), n=1000 d=10, "
+                                        "65,536 chains"),
 }
 
 
@@ -63,7 +69,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--d", type=int, default=None)
     p.add_argument("--chains", type=int, default=None, help="chains per GPU")
-    p.add_argument("--sampler", default=None, choices=["rwm", "mala", "hmc", "hmcda"])
+    p.add_argument("--sampler", default=None, choices=["rwm", "mala", "hmc", "hmcda", "ram"])
     p.add_argument("--thinning", type=int, default=None)
     p.add_argument("--spl", type=int, default=-1, help="steps per launch (0: whole run in one launch; "
                                                        "-1: default of the library)")
@@ -99,6 +105,8 @@ def build_model(mc, cfg, d):
 def build_sampler(mc, cfg, name):
     if cfg["model"] == "logistic" and name == "mala":
         return mc.MALA(0.001)                        # test/test_syntax.jl:28
+    if name == "ram":
+        return mc.RAM(1.0, 0.3) if cfg["model"] == "linear" else mc.RAM(1.0, 0.234)
     return {"rwm": lambda: mc.RWM(0.1), "mala": lambda: mc.MALA(0.1), "hmc": lambda: mc.HMC(10, 0.1),
             "hmcda": lambda: mc.HMCDA()}[name]()
 
@@ -107,7 +115,9 @@ def hbm_bytes_per_unit(d, sampler):
     """SURVEY.md §8(d) algorithmic bytes per chain-step (state round trip + 1 accept bit) and per kept
     chain-step (sample, + gradient for gradient samplers)."""
     per_step = (32 * d if sampler == "mala" else 16 * d) + 16 + 1 / 8
-    per_kept = 8 * d * (1 if sampler == "rwm" else 2)
+    if sampler == "ram":                 # + the jump factor S read and written back (d(d+1)/2 doubles)
+        per_step += 8 * d * (d + 1)
+    per_kept = 8 * d * (1 if sampler in ("rwm", "ram") else 2)
     return per_step, per_kept
 
 
@@ -182,7 +192,7 @@ def main():
     dev = torch.device("cuda", local)
     nkept = len(runner.r)
     samples = torch.empty((nkept, d, C), dtype=torch.float64, device=dev)
-    grad_sampler = args.sampler != "rwm"
+    grad_sampler = args.sampler not in ("rwm", "ram")
     grads = torch.empty((nkept, d, C), dtype=torch.float64, device=dev) if grad_sampler else None
     bits = torch.empty((nkept, (C + 63) // 64), dtype=torch.int64, device=dev)
     out = _lib.Outputs()

@@ -84,7 +84,7 @@ enum {
 };
 
 /* samplers */
-enum { MCMC_RWM = 1, MCMC_MALA = 2, MCMC_HMC = 3, MCMC_HMCDA = 4 };
+enum { MCMC_RWM = 1, MCMC_MALA = 2, MCMC_HMC = 3, MCMC_HMCDA = 4, MCMC_RAM = 5 };
 
 typedef struct mcmc_ctx mcmc_ctx;
 typedef struct mcmc_model mcmc_model;
@@ -108,12 +108,12 @@ typedef struct {
 } mcmc_model_desc;
 
 typedef struct {
-    int32_t kind;            /* MCMC_RWM | MCMC_MALA | MCMC_HMC | MCMC_HMCDA                      */
-    double scale;            /* RWM: scale (RWM.jl:25)                                             */
+    int32_t kind;            /* MCMC_RWM | MCMC_MALA | MCMC_HMC | MCMC_HMCDA | MCMC_RAM           */
+    double scale;            /* RWM, RAM: scale (RWM.jl:25, RAM.jl:23)                             */
     double drift_step;       /* MALA: driftStep (MALA.jl:51)                                       */
     int64_t n_leaps;         /* HMC: nLeaps (HMC.jl:54)                                            */
     double leap_step;        /* HMC: leapStep (HMC.jl:55)                                          */
-    double rate, len, shrinkage, t0, step;   /* HMCDA (HMCDA.jl:25-29)                             */
+    double rate, len, shrinkage, t0, step;   /* HMCDA (HMCDA.jl:25-29); rate: RAM target rate (RAM.jl:24) */
     int32_t tuner;           /* 0: nothing; 1: EmpiricalMCMCTuner (MALA, HMC)                      */
     int64_t adapt_step, max_step;            /* EmpMCTuner (samplers.jl:33-37)                      */
     double target_path, target_rate;
@@ -183,6 +183,10 @@ int mcmc_chains_steps_done(mcmc_chains* chains, int64_t* steps);
  * create/reset: steps x C for RWM/MALA, the leapfrog count for HMC/HMCDA (HMC.jl:219-228),
  * whose trajectory length varies per chain under HMCDA / EmpMCTuner. */
 int mcmc_chains_evals(mcmc_chains* chains, int64_t* evals);
+/* RAM: the current jump factor S of every chain (RAM.jl:55, :81), lower triangle packed by rows:
+ * element (r, c), c <= r, of chain k at S[(r(r+1)/2 + c) * nchains + k]; host buffer of
+ * d(d+1)/2 * nchains doubles.  MCMC_E_INVALID_ARG for other samplers. */
+int mcmc_chains_ram_factor(mcmc_chains* chains, double* S);
 /* steps fused per kernel launch (0 = whole run in one launch, the default). */
 int mcmc_chains_set_steps_per_launch(mcmc_chains* chains, int64_t steps_per_launch);
 /* store gradients of kept samples for gradient samplers (default 1, SerialMC.jl:51-53) */

@@ -10,7 +10,7 @@ enum DistKind : int32_t {
     DK_NORMAL = 1, DK_UNIFORM = 2, DK_WEIBULL = 3, DK_BETA = 4, DK_TDIST = 5, DK_EXPONENTIAL = 6, DK_GAMMA = 7,
     DK_CAUCHY = 8, DK_LOGNORMAL = 9, DK_LAPLACE = 10
 };
-enum SamplerKind : int32_t { SK_RWM = 1, SK_MALA = 2, SK_HMC = 3, SK_HMCDA = 4 };
+enum SamplerKind : int32_t { SK_RWM = 1, SK_MALA = 2, SK_HMC = 3, SK_HMCDA = 4, SK_RAM = 5 };
 
 // Model parameters as the kernels see them (device pointers).
 struct ModelArgs {
@@ -54,6 +54,8 @@ struct ChainState {
     int32_t* t_leaps;           // HMC tuned nLeaps
     int32_t* t_acc;             // tuner accepted counter
     int32_t* t_prop;            // tuner proposed counter
+    double* ram_L;              // RAM: jump factor S, two halves of packed padded rows [dpad(dpad+1)/2][ram_ld]
+    int64_t ram_ld;             // RAM: chain stride of ram_L (a multiple of 256)
 };
 
 // One launch of the fused step kernel.

@@ -84,6 +84,8 @@ struct mcmc_chains {
     Layout layout = LAYOUT_LPC;
     ChainState st{};
     double* d_scale_eff = nullptr;   // model.scale .* sampler.scale (RWM.jl:52)
+    std::vector<double> h_scale_eff; // its host copy
+    int ram_dpad = 0;                // RAM: padded factor width
     double scale1 = 0.0;             // its common value when all coordinates agree
     int32_t scale_uniform = 0;
     double* d_init_x = nullptr;      // optional per-chain start, [d][C]
@@ -205,6 +207,16 @@ extern "C" int mcmc_sampler_validate(const mcmc_sampler_cfg* s) {
             if (!(s->n_leaps > 0)) return fail(MCMC_E_INVALID_ARG, "inner steps should be > 0");        // HMC.jl:60
             if (!(s->leap_step > 0)) return fail(MCMC_E_INVALID_ARG, "inner steps scaling should be > 0"); // HMC.jl:61
             break;
+        case MCMC_RAM: {
+            if (!(s->scale > 0)) return fail(MCMC_E_INVALID_ARG, "scale should be > 0");               // RAM.jl:27
+            if (!(s->rate > 0.0 && s->rate < 1.0)) {
+                char buf[160];
+                snprintf(buf, sizeof buf, "target acceptance rate (%g) should be between 0 and 1", s->rate);
+                return fail(MCMC_E_INVALID_ARG, buf);                                                    // RAM.jl:28
+            }
+            if (s->tuner) return fail(MCMC_E_UNSUPPORTED, "RAM takes no tuner");
+            break;
+        }
         case MCMC_HMCDA: {
             char buf[160];
             if (!(0.0 < s->rate && s->rate < 1.0)) {
@@ -413,6 +425,10 @@ static bool model_is_glm(const mcmc_model* m) { return m->args.kind == MK_LOGIST
 
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
+// RAM jump factor (ram.hpp): packed lower-triangular rows padded to the kernel's width + a trash row,
+// two halves
+static size_t ram_nrows(int d) { return (size_t)d * (size_t)(d + 1) / 2; }
+
 // State layout of a chain batch: lane-per-chain [d][ld] for d <= 32, wave-per-chain [C][ld] above.
 static Layout layout_for(const mcmc_model* m) {
     if (model_is_glm(m)) return LAYOUT_GLM;
@@ -498,7 +514,7 @@ extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, 
 static void free_state(mcmc_chains* c) {
     ChainState& s = c->st;
     dfree(s.x); dfree(s.lp); dfree(s.g); dfree(s.t_step); dfree(s.t_bar); dfree(s.t_h);
-    dfree(s.t_leaps); dfree(s.t_acc); dfree(s.t_prop);
+    dfree(s.t_leaps); dfree(s.t_acc); dfree(s.t_prop); dfree(s.ram_L);
     s = ChainState{};
 }
 
@@ -532,6 +548,15 @@ static int init_state(mcmc_chains* c) {
         HIP_TRY(mcmc_fill_f64(c->st.t_bar, c->C, 1.0, st));     // dualLeapStep = 1.
         HIP_TRY(mcmc_fill_f64(c->st.t_h, c->C, 0.0, st));       // dualH = 0.
     }
+    if (sa.kind == SK_RAM) {
+        // S = diag(model.scale .* sampler.scale) (RAM.jl:51,55) in half 0: packed rows, diagonal (r, r)
+        // at r(r+1)/2 + r; the padding block d..dpad-1 is the identity
+        const int64_t rl = c->st.ram_ld;
+        HIP_TRY(hipMemsetAsync(c->st.ram_L, 0, 2 * (ram_nrows(c->ram_dpad) + 1) * (size_t)rl * 8, st));
+        for (int r = 0; r < c->ram_dpad; ++r)
+            HIP_TRY(mcmc_fill_f64(c->st.ram_L + (size_t)(r * (r + 1) / 2 + r) * rl, rl,
+                                  r < d ? c->h_scale_eff[r] : 1.0, st));
+    }
     if (sa.tuner) {
         HIP_TRY(mcmc_fill_i32(c->st.t_acc, c->C, 0, st));
         HIP_TRY(mcmc_fill_i32(c->st.t_prop, c->C, 0, st));
@@ -552,7 +577,9 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (nchains <= 0) return fail(MCMC_E_INVALID_ARG, "nchains should be > 0");
     if (chain_offset < 0 || chain_offset + nchains > (int64_t)0x100000000LL)
         return fail(MCMC_E_INVALID_ARG, "global chain ids must fit in 32 bits");
-    if (s->kind != MCMC_RWM && !m->has_gradient) {
+    if (s->kind == MCMC_RAM && m->args.d > 32)
+        return fail(MCMC_E_UNSUPPORTED, "RAM is built for d <= 32 (the d x d jump factor of every chain is kept in HBM)");
+    if (s->kind != MCMC_RWM && s->kind != MCMC_RAM && !m->has_gradient) {
         const char* nm = s->kind == MCMC_MALA ? "MALA" : s->kind == MCMC_HMC ? "HMC" : "HMCDA";
         return fail(MCMC_E_NEEDS_GRADIENT, std::string(nm) + " sampler requires model with gradient function");
     }
@@ -611,8 +638,15 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     }
     // scale = model.scale .* sampler.scale (RWM.jl:52); other samplers do not use it.
     std::vector<double> se(m->scale);
-    if (sa.kind == SK_RWM)
+    if (sa.kind == SK_RWM || sa.kind == SK_RAM)                       // RAM.jl:51
         for (auto& v : se) v = v * sa.scale;
+    c->h_scale_eff = se;
+    if (sa.kind == SK_RAM) {
+        // padded width: the lane-per-chain kernel's NC = 4 ceil(d/4), the regression kernel's DF = d_pad
+        c->ram_dpad = c->layout == LAYOUT_GLM ? mcmc_glm_d_pad(d) : (int)round_up(d, 4);
+        c->st.ram_ld = round_up(nchains, 256);
+        if (int r = dmalloc(&c->st.ram_L, 2 * (ram_nrows(c->ram_dpad) + 1) * (size_t)c->st.ram_ld)) return bail(r);
+    }
     c->scale1 = se.empty() ? 0.0 : se[0];
     c->scale_uniform = 1;
     for (double v : se)
@@ -668,6 +702,20 @@ extern "C" int mcmc_chains_evals(mcmc_chains* c, int64_t* evals) {
     return MCMC_OK;
 }
 
+extern "C" int mcmc_chains_ram_factor(mcmc_chains* c, double* S) {
+    if (!c || !S) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    if (c->sa.kind != SK_RAM) return fail(MCMC_E_INVALID_ARG, "chains do not run the RAM sampler");
+    mcmc_ctx* ctx = c->model->ctx;
+    if (int r = set_device(ctx)) return r;
+    const size_t rows = ram_nrows(c->model->args.d);          // the leading rows of the padded packing
+    const size_t rl = (size_t)c->st.ram_ld;
+    const double* cur = c->st.ram_L + (size_t)(c->steps_done & 1) * (ram_nrows(c->ram_dpad) + 1) * rl;   // written last
+    HIP_TRY(hipMemcpy2DAsync(S, (size_t)c->C * 8, cur, rl * 8, (size_t)c->C * 8, rows,
+                             hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MCMC_OK;
+}
+
 extern "C" int mcmc_chains_steps_done(mcmc_chains* c, int64_t* steps) {
     if (!c || !steps) return fail(MCMC_E_INVALID_ARG, "NULL argument");
     *steps = c->steps_done;
@@ -702,7 +750,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     if (c->steps_done + r->len > 0xffffffffLL) return fail(MCMC_E_INVALID_ARG, "step counter exceeds 2^32");
     const bool on_dev = out && out->on_device;
     const bool want_samples = out && out->samples;
-    const bool grad_sampler = c->sa.kind != SK_RWM;
+    const bool grad_sampler = c->sa.kind != SK_RWM && c->sa.kind != SK_RAM;   // RWM, RAM: no gradients
     const bool want_grads = out && out->gradients && grad_sampler && c->store_grads;
     const bool want_bits = out && out->accept_bits;
 

@@ -23,6 +23,7 @@
 #include "../common.hpp"
 #include "../detmath.hpp"
 #include "../models.hpp"
+#include "../ram.hpp"
 #include "../host/kernels_api.hpp"
 
 namespace mcmc {
@@ -463,6 +464,120 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_rwm(GlmArgs a) {
     glm_count_evals(a, p, s.nsteps);
 }
 
+// RAM (RAM.jl:56-82) for d <= 32 (one d-slice, NW = 1), the factor padded to DF = 16 NM (ram.hpp).
+// Row r of S belongs to the lane that owns coordinate r (own_coord): it forms u[r] = (S z)[r] from the
+// full normal vector (every lane of the chain draws all DF/4 blocks), keeps it across the evaluation,
+// and after the accept updates its rows of every column k; the pivot u[k] comes from its owner by a
+// cross-lane read.  Rows r <= k of a column compute throw-away values whose stores go to the trash row
+// of the half (index ram_rows(DF)), so the loop carries no branches.
+template <int NM, int NW>
+__global__ __launch_bounds__(glm_block<NW>()) void glm_ram(GlmArgs a) {
+    static_assert(NW == 1, "RAM on regression targets is built for d <= 32");
+    constexpr int DF = 16 * NM;
+    constexpr int NS = 4 * NM;                                          // own coordinates per lane
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const StepArgs& s = a.s;
+    const GlmPos p = glm_pos(a);
+    const GlmLds L = glm_lds(a, smem);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    f64x4 dummy[NM];
+    double* const Lc = a.st.ram_L + p.c;                        // own column (padding past the last chain)
+    const uint64_t ld = (uint64_t)a.st.ram_ld;
+    const int d = s.d;
+    double lp = a.st.lp[p.live ? p.c : 0];
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        double xp[NS], u[NS], nz = 0.0;
+        {
+            double z[DF];
+#pragma unroll
+            for (int b = 0; b < DF / 4; ++b) {                                  // rvec = randn(d)
+                const u32x4 w = rs.block(chain, (uint32_t)i, (uint32_t)b, TAG_NORMAL);
+                normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3]);
+            }
+#pragma unroll
+            for (int k = 0; k < DF; ++k) {
+                if (k >= d) z[k] = 0.0;                                         // padding: identity block
+                nz = __builtin_fma(z[k], z[k], nz);                             // dot(rvec, rvec)
+            }
+            double x[NS];
+            glm_load<NM>(a, p, a.st.x, x);
+            const uint64_t ldo = ram_opaque(ld);
+            const double* Ls = ram_half<DF>(Lc, i - 1, ldo);
+#pragma unroll
+            for (int slot = 0; slot < NS; ++slot) {
+                // own row r: the fma chain over c <= r, then exact no-ops fma(0, z, acc)
+                const int r = own_coord(p, slot);
+                const double* Lr = Ls + (uint64_t)(r * (r + 1) / 2) * ldo;
+                double acc = 0.0;
+#pragma unroll
+                for (int c = 0; c < DF; ++c) {
+                    const double v = Lr[(uint64_t)c * ldo];
+                    acc = __builtin_fma(c <= r ? v : 0.0, z[c], acc);
+                }
+                u[slot] = acc;
+                xp[slot] = x[slot] + acc;                                     // RAM.jl:60
+                __builtin_amdgcn_sched_barrier(0);                            // one row's loads at a time
+            }
+        }
+        bool oos;
+        const double lpp = glm_eval<NM, NW, false>(a, p, L, xp, dummy, oos);
+        const double ratio = lpp - lp;
+        const bool acc = glm_mh_short_circuit(rs, chain, (uint32_t)i, ratio);
+        if (acc) {
+            glm_store<NM>(a, p, a.st.x, s.ld, xp);
+            lp = lpp;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            if (!acc) glm_load<NM>(a, p, a.st.x, xp);
+            glm_store_kept<NM>(a, p, kk, s.samples, xp);
+            glm_store_bit(a, p, kk, acc);
+        }
+        // S <- chol(S S' + beta u u')' (ram.hpp ram_update, distributed over the chain's four lanes)
+        const double beta = ram_alpha(i, d, ratio, a.sa.rate) / nz;
+        const bool up = beta >= 0.0;
+        const double sb = __builtin_sqrt(__builtin_fabs(beta));
+#pragma unroll
+        for (int slot = 0; slot < NS; ++slot) u[slot] = sb * u[slot];
+        const uint64_t ldu = ram_opaque(ld);
+        const double* Ls = ram_half<DF>(Lc, i - 1, ldu);
+        double* Ld = ram_half<DF>(Lc, i, ldu);
+        const uint64_t trash = (uint64_t)ram_rows(DF) * ldu;
+#pragma unroll
+        for (int k = 0; k < DF; ++k) {
+            const int kslot = 4 * (k >> 4) + (k & 3);                           // owner: q = (k & 15) >> 2
+            const double xk = __shfl(u[kslot], p.cl + 16 * ((k & 15) >> 2), 64);
+            const uint64_t okk = (uint64_t)(k * (k + 1) / 2 + k) * ldu;
+            const double lkk = Ls[okk];
+            const double t2 = xk * xk;
+            const double l2 = lkk * lkk;
+            const double r = __builtin_sqrt(up ? l2 + t2 : l2 - t2);
+            const double cc = r / lkk;
+            const double sn = xk / lkk;
+            const double ic = 1.0 / cc;
+            Ld[okk] = r;
+#pragma unroll
+            for (int slot = 0; slot < NS; ++slot) {
+                const int q = own_coord(p, slot);
+                if (16 * (slot >> 2) + 12 + (slot & 3) <= k) continue;          // no row of this slot is below k
+                const bool below = q > k;
+                const uint64_t oq = (uint64_t)(q * (q + 1) / 2 + k) * ldu;     // in bounds for q <= k too
+                const double l0 = Ls[oq];
+                const double su = sn * u[slot];
+                const double l = (up ? l0 + su : l0 - su) * ic;
+                Ld[below ? oq : trash] = l;
+                const double un = cc * u[slot] - sn * l;
+                u[slot] = below ? un : u[slot];
+            }
+            __builtin_amdgcn_sched_barrier(0);                                  // one column's loads at a time
+        }
+    }
+    if (p.live && p.q == 0 && p.slice == 0) a.st.lp[p.c] = lp;
+    glm_count_evals(a, p, s.nsteps);
+}
+
 template <int NM, int NW>
 __global__ __launch_bounds__(glm_block<NW>()) void glm_mala(GlmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -729,6 +844,12 @@ static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hip
         case SK_MALA: glm_mala<NM, NW><<<grid, B, lds, st>>>(a); break;
         case SK_HMC: glm_hmc<NM, NW, false><<<grid, B, lds, st>>>(a); break;
         case SK_HMCDA: glm_hmc<NM, NW, true><<<grid, B, lds, st>>>(a); break;
+        case SK_RAM:
+            if constexpr (NW == 1 && NM <= 2) {
+                glm_ram<NM, NW><<<grid, B, lds, st>>>(a);
+                break;
+            }
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

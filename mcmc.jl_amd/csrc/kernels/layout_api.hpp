@@ -15,3 +15,8 @@ MCMC_LAYOUT_UNIT_DECL(wpc, iso)
 MCMC_LAYOUT_UNIT_DECL(wpc, normal)
 MCMC_LAYOUT_UNIT_DECL(wpc, absnormal)
 MCMC_LAYOUT_UNIT_DECL(wpc, dist)
+// lane-per-chain RAM kernels (lpc_ram_a.hip, lpc_ram_b.hip)
+hipError_t mcmc_lpc_ram_iso(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_lpc_ram_normal(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_lpc_ram_absnormal(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_lpc_ram_dist(const mcmc::KernelArgs& a, hipStream_t st);

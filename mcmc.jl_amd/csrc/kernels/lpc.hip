@@ -5,6 +5,15 @@
 hipError_t mcmc_launch_lpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
     using namespace mcmc;
     if (a.s.d < 1 || a.s.d > 32) return hipErrorInvalidValue;
+    if (a.sa.kind == SK_RAM) {
+        switch (a.m.kind) {
+            case MK_ISO: return mcmc_lpc_ram_iso(a, st);
+            case MK_NORMAL: return mcmc_lpc_ram_normal(a, st);
+            case MK_ABS_NORMAL: return mcmc_lpc_ram_absnormal(a, st);
+            case MK_DIST: return mcmc_lpc_ram_dist(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (a.m.kind) {
         case MK_ISO: return mcmc_lpc_step_iso(a, st);
         case MK_NORMAL: return mcmc_lpc_step_normal(a, st);

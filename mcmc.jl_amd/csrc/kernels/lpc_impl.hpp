@@ -87,3 +87,33 @@ static hipError_t lpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
                                     int check, hipStream_t st) {                                         \
         return mcmc::lpc_eval_m<mcmc::Model>(a, xin, lp, g, check, st);                                 \
     }
+
+// RAM kernels live in their own translation units (lpc_ram_*.hip, built without machine LICM: hoisted
+// fp64 constants would pin the scalar file the factor addressing needs); LPC_RAM_UNIT(iso, IsoDot)
+// defines mcmc_lpc_ram_iso.
+namespace mcmc {
+template <int NB, class M>
+__global__ __launch_bounds__(kBlock, NB <= 4 ? 2 : 1) void lpc_ram(KernelArgs a) { ram_body<LaneChain<NB, false>, M>(a); }
+
+template <class M>
+static hipError_t lpc_ram_step(const KernelArgs& a, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    switch ((a.s.d + 3) / 4) {
+        case 1: lpc_ram<1, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 2: lpc_ram<2, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 3: lpc_ram<3, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 4: lpc_ram<4, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 5: lpc_ram<5, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 6: lpc_ram<6, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 7: lpc_ram<7, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 8: lpc_ram<8, M><<<grid, kBlock, 0, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+}  // namespace mcmc
+
+#define LPC_RAM_UNIT(name, Model)                                                \
+    hipError_t mcmc_lpc_ram_##name(const mcmc::KernelArgs& a, hipStream_t st) { \
+        return mcmc::lpc_ram_step<mcmc::Model>(a, st);                          \
+    }

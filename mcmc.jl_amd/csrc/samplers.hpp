@@ -26,6 +26,7 @@
 #include "common.hpp"
 #include "detmath.hpp"
 #include "models.hpp"
+#include "ram.hpp"
 #include "host/kernels_api.hpp"
 
 namespace mcmc {
@@ -492,6 +493,67 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
         p.store_t(a.st.t_acc, n_acc);
         p.store_t(a.st.t_prop, n_prop);
     }
+}
+
+// ------------------------------------------------------------------ RAM
+// Robust adaptive Metropolis (RAM.jl:39-83), lane per chain.  x' = x + S z, RWM accept, then the
+// jump factor S (packed rows in HBM, ram.hpp) takes the rank-1 update of RAM.jl:77-81.
+template <class P, class M>
+__device__ __forceinline__ void ram_body(const KernelArgs& a) {
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const P p(s);
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    constexpr int NC = P::NC;
+    double x[NC];
+    p.load(a.st.x, s.ld, x);
+    double lp = p.load_scalar(a.st.lp);
+    const uint32_t col = (uint32_t)p.c;                        // own column (padding past the last chain)
+    const uint64_t ld = (uint64_t)a.st.ram_ld;
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        const uint64_t ldo = ram_opaque(ld);
+        double u[NC], nz = 0.0;
+        {
+            double z[NC];
+            gen_normals(p, rs, chain, (uint32_t)i, z);                          // rvec = randn(d)
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                if (!p.valid(k)) z[k] = 0.0;                                    // padding: identity block
+                nz = __builtin_fma(z[k], z[k], nz);                             // dot(rvec, rvec)
+            }
+            ram_matvec<NC>(ram_half<NC>(a.st.ram_L, i - 1, ldo), col, ldo, z, u);   // S * rvec
+        }
+        double lpp;
+        {
+            double xp[NC];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) xp[k] = x[k] + u[k];                 // RAM.jl:60
+            bool oos;
+            lpp = eval_lp(p, model, xp, oos);
+        }
+        const double ratio = lpp - lp;
+        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        if (acc) {
+            // the proposal is recomputed (bitwise the same sums) rather than held across the evaluation
+#pragma unroll
+            for (int k = 0; k < NC; ++k) x[k] = x[k] + u[k];
+            lp = lpp;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            p.store_kept(s, kk, x, s.samples);
+            p.store_bit(s, kk, acc);
+        }
+        const uint64_t ldu = ram_opaque(ld);       // fresh: no offset products live across the evaluation
+        ram_update<NC>(ram_half<NC>(a.st.ram_L, i - 1, ldu), ram_half<NC>(a.st.ram_L, i, ldu), col, ldu,
+                       ram_alpha(i, s.d, ratio, sa.rate), nz, u);
+    }
+    p.store(a.st.x, s.ld, x);
+    p.store_t(a.st.lp, lp);
+    p.count_evals(s, s.nsteps);
 }
 
 // ------------------------------------------------------------------ eval

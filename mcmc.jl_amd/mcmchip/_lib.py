@@ -36,6 +36,7 @@ SAMPLER_RWM = 1
 SAMPLER_MALA = 2
 SAMPLER_HMC = 3
 SAMPLER_HMCDA = 4
+SAMPLER_RAM = 5
 
 VAR_IMSE = 1
 VAR_IPSE = 2
@@ -47,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_model_create", "mcmc_model_destroy", "mcmc_model_eval",
     "mcmc_sampler_validate", "mcmc_runner_validate",
     "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done", "mcmc_chains_evals",
+    "mcmc_chains_ram_factor",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients",
     "mcmc_run_serialmc", "mcmc_seqmc_validate", "mcmc_run_seqmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
 )
@@ -109,6 +111,13 @@ def load() -> ct.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libmcmc_hip.so not found at {LIB_PATH}: run __graft_entry__.build() "
                           "(make -C mcmc.jl_amd) first")
+    # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's): import it first when present so
+    # one HIP runtime serves both torch tensors and this library.  Loading /opt/rocm's runtime first
+    # leaves a later torch without devices ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ct.CDLL(LIB_PATH)
     P = ct.c_void_p
     pp = ct.POINTER(ct.c_void_p)
@@ -131,6 +140,7 @@ def load() -> ct.CDLL:
         "mcmc_chains_reset": (ct.c_int, [P]),
         "mcmc_chains_steps_done": (ct.c_int, [P, ct.POINTER(i64)]),
         "mcmc_chains_evals": (ct.c_int, [P, ct.POINTER(i64)]),
+        "mcmc_chains_ram_factor": (ct.c_int, [P, ct.c_void_p]),
         "mcmc_chains_set_steps_per_launch": (ct.c_int, [P, i64]),
         "mcmc_chains_set_store_gradients": (ct.c_int, [P, i32]),
         "mcmc_run_serialmc": (ct.c_int, [P, ct.POINTER(RunnerCfg), ct.POINTER(Outputs)]),

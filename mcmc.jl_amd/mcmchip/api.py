@@ -3,7 +3,7 @@
 Names, argument meaning and error behaviour follow the reference:
 
   model(f; init, scale, grad)    src/modellers/mcmcmodels.jl:27-33, likmodel.jl:100-143
-  RWM, MALA, HMC, HMCDA          src/samplers/{RWM,MALA,HMC,HMCDA}.jl (constructors + @asserts)
+  RWM, MALA, HMC, HMCDA, RAM     src/samplers/{RWM,MALA,HMC,HMCDA,RAM}.jl (constructors + @asserts)
   EmpMCTuner                     src/samplers/samplers.jl:32-50
   SerialMC(steps, burnin, thinning) / SerialMC(range)   src/runners/SerialMC.jl:12-35
   m * s * r -> MCMCTask          src/MCMC.jl:87-98
@@ -31,7 +31,7 @@ from ._lib import check, dptr
 
 __all__ = [
     "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
-    "RWM", "MALA", "HMC", "HMCDA", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
+    "RWM", "MALA", "HMC", "HMCDA", "RAM", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
     "run", "resume", "device_count",
 ]
 
@@ -249,6 +249,7 @@ EmpMCTuner = EmpiricalMCMCTuner
 class _Sampler:
     kind = 0
     tuner = None
+    uses_gradient = True       # MALA, HMC, HMCDA need model.evalg; RWM and RAM do not
 
     def cfg(self) -> _lib.SamplerCfg:
         c = _lib.SamplerCfg()
@@ -267,6 +268,7 @@ class _Sampler:
 class RWM(_Sampler):
     """Random-walk Metropolis (RWM.jl:24-36)."""
     kind = _lib.SAMPLER_RWM
+    uses_gradient = False
 
     def __init__(self, scale: float = 1.0, tuner=None):
         if not scale > 0:
@@ -364,6 +366,25 @@ class HMCDA(_Sampler):
         return c
 
 
+class RAM(_Sampler):
+    """Robust adaptive Metropolis (RAM.jl:22-34): RAM(), RAM(scale), RAM(scale, rate),
+    RAM(scale=..., rate=...).  Each chain adapts its own d x d jump factor (kept on the device)."""
+    kind = _lib.SAMPLER_RAM
+    uses_gradient = False
+
+    def __init__(self, scale: float = 1.0, rate: float = 0.234):
+        if not scale > 0:
+            raise AssertionError("scale should be > 0")                                           # RAM.jl:27
+        if not (rate > 0.0 and rate < 1.0):
+            raise AssertionError(f"target acceptance rate ({rate}) should be between 0 and 1")   # RAM.jl:28
+        self.scale, self.rate = float(scale), float(rate)
+
+    def cfg(self):
+        c = super().cfg()
+        c.scale, c.rate = self.scale, self.rate
+        return c
+
+
 # ------------------------------------------------------------------ runner
 class SerialMC:
     """SerialMC runner (SerialMC.jl:12-35): keeps samples i in r = (burnin+1):thinning:steps."""
@@ -428,7 +449,7 @@ class MCMCTask:
         self._h = None
         if not isinstance(runner, SerialMC) and type(runner).__name__ != "SeqMC":
             raise NotImplementedError("runners: SerialMC (one batch) or SeqMC (lists of targets, run_seqmc)")
-        if sampler.kind != _lib.SAMPLER_RWM and not model.has_gradient:
+        if sampler.uses_gradient and not model.has_gradient:
             name = type(sampler).__name__
             raise AssertionError(f"{name} sampler requires model with gradient function")
         self.model, self.sampler, self.runner = model, sampler, runner
@@ -474,6 +495,15 @@ class MCMCTask:
         v = ct.c_int64(0)
         check(_lib.load().mcmc_chains_evals(self._h, ct.byref(v)))
         return v.value
+
+    def ram_factor(self) -> np.ndarray:
+        """RAM: the current jump factor S of every chain as [nchains][d][d] lower-triangular matrices."""
+        if self._h is None:
+            raise AssertionError("the task has not run")
+        d, C = self.model.size, self.nchains
+        packed = np.empty((d * (d + 1) // 2, C))
+        check(_lib.load().mcmc_chains_ram_factor(self._h, packed.ctypes.data))
+        return unpack_ram_factor(packed, d)
 
     def reset(self) -> None:
         if self._h is not None:
@@ -525,6 +555,15 @@ class MCMCChain:
         return f"{d} parameters, {nk} samples (per parameter), {C} chain(s), {round(self.runTime, 1)} sec."
 
 
+def unpack_ram_factor(packed: np.ndarray, d: int) -> np.ndarray:
+    """[d(d+1)/2][C] packed lower rows -> [C][d][d]."""
+    C = packed.shape[1]
+    S = np.zeros((C, d, d))
+    r, c = np.tril_indices(d)                                  # row-major order of the packed rows
+    S[:, r, c] = packed.T
+    return S
+
+
 def _unpack_bits(bits: np.ndarray, C: int) -> np.ndarray:
     """[nkept][ceil(C/64)] u64 -> bool [C, nkept]; bit c%64 of word c//64 is chain c."""
     nk = bits.shape[0]
@@ -540,7 +579,7 @@ def _run_task(t: MCMCTask) -> MCMCChain:
     nk = len(r.r)
     nw = (C + 63) // 64
     samples = np.empty((nk, d, C))
-    grads = np.empty((nk, d, C)) if t.sampler.kind != _lib.SAMPLER_RWM else None
+    grads = np.empty((nk, d, C)) if t.sampler.uses_gradient else None
     bits = np.zeros((nk, nw), dtype=np.uint64)
     fx = np.empty((d, C))
     flp = np.empty(C)

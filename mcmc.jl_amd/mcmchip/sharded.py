@@ -81,7 +81,7 @@ def run_sharded(model, sampler, runner: SerialMC, nchains: int, seed: int = 1, g
     d = model.size
     nk = len(runner.r)
     dev = torch.device("cuda", device)
-    grad = sampler.kind != _lib.SAMPLER_RWM
+    grad = sampler.uses_gradient
     parts = {
         "samples": torch.empty((nk, d, max(cnt, 1)), dtype=torch.float64, device=dev),
         "gradients": torch.empty((nk, d, max(cnt, 1)), dtype=torch.float64, device=dev) if grad else None,

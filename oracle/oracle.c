@@ -36,6 +36,7 @@
 #define ORC_MALA 2
 #define ORC_HMC 3
 #define ORC_HMCDA 4
+#define ORC_RAM 5
 
 typedef struct {
     int32_t kind;
@@ -73,6 +74,7 @@ typedef struct {
     int32_t* t_acc;
     int32_t* t_prop;
     int64_t* n_evals;   /* log-target evaluations per chain (steps for RWM/MALA, leapfrogs for HMC) */
+    double* ram_L;      /* RAM jump factor S: packed lower rows, element (r, c) at [r(r+1)/2 + c][nchains] */
 } orc_state;
 
 static const double ORC_LOG2PI = 0x1.d67f1c864beb5p+0;
@@ -429,6 +431,38 @@ static double orc_trajectory(const orc_model* m, double eps, int64_t nl, double*
     return lp;
 }
 
+/* RAM scale tuning (RAM.jl:77-81) on the packed factor Lc (element (r, c) at Lc[(r(r+1)/2 + c) * C]).
+   The reference sets S = chol(S (I + a z z'/|z|^2) S')'; restated as the rank-1 Cholesky update
+   (a >= 0) / downdate (a < 0) of S with sqrt(|a|/|z|^2) u, u = S z, in the kernels' order
+   (mcmc.jl_amd/csrc/ram.hpp ram_update). */
+static void orc_ram_update(double* Lc, int64_t C, int d, int64_t i, double ratio, double rate, double nz, double* u) {
+    const double eta = fmin(1.0, (double)d * orc_exp((-2.0 / 3.0) * orc_log((double)i)));
+    const double alpha = eta * (fmin(1.0, orc_exp(ratio)) - rate);
+    const double beta = alpha / nz;
+    const int up = beta >= 0.0;
+    const double sb = sqrt(fabs(beta));
+    for (int k = 0; k < d; ++k) u[k] = sb * u[k];
+    for (int k = 0; k < d; ++k) {
+        double* Lkk = Lc + (size_t)(k * (k + 1) / 2 + k) * C;
+        const double lkk = *Lkk;
+        const double xk = u[k];
+        const double t2 = xk * xk;
+        const double l2 = lkk * lkk;
+        const double r = sqrt(up ? l2 + t2 : l2 - t2);
+        const double cc = r / lkk;
+        const double sn = xk / lkk;
+        const double ic = 1.0 / cc;
+        *Lkk = r;
+        for (int q = k + 1; q < d; ++q) {
+            double* Lq = Lc + (size_t)(q * (q + 1) / 2 + k) * C;
+            const double su = sn * u[q];
+            const double l = (up ? *Lq + su : *Lq - su) * ic;
+            *Lq = l;
+            u[q] = cc * u[q] - sn * l;
+        }
+    }
+}
+
 /* ------------------------------------------------------------ one chain */
 /* `len` steps of SerialMC (SerialMC.jl:47-67) for chain c, sampler loop counter continuing from step0. */
 static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, uint32_t chain, int64_t c,
@@ -462,6 +496,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
     for (int64_t t = 0; t < len; ++t) {
         const int64_t i = step0 + t + 1;      /* the sampler's loop counter (HMC.jl:252 `for i in 1:Inf`) */
         int acc = 0;
+        double ram_ratio = 0.0, ram_nz = 0.0;
         double p_da = 0.0;
         if (s->kind == ORC_RWM) {
             /* RWM.jl:58-71 */
@@ -474,6 +509,27 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 memcpy(x, xp, sizeof(double) * d);
                 lp = lpp;
             }
+        } else if (s->kind == ORC_RAM) {
+            /* RAM.jl:58-81 */
+            double* Lc = st->ram_L + c;
+            orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* rvec = randn(d) */
+            double nz = 0.0;
+            for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);         /* dot(rvec, rvec) */
+            for (int r = 0; r < d; ++r) {                                     /* S * rvec */
+                double a = 0.0;
+                for (int q = 0; q <= r; ++q) a = fma(Lc[(size_t)(r * (r + 1) / 2 + q) * C], mom[q], a);
+                gp[r] = a;
+            }
+            for (int j = 0; j < d; ++j) xp[j] = x[j] + gp[j];
+            double lpp = orc_eval(m, xp, NULL, tmp, order);
+            double ratio = lpp - lp;
+            acc = orc_mh_short_circuit(seed, chain, (uint32_t)i, ratio);
+            if (acc) {
+                memcpy(x, xp, sizeof(double) * d);
+                lp = lpp;
+            }
+            ram_ratio = ratio;
+            ram_nz = nz;
         } else if (s->kind == ORC_MALA) {
             /* MALA.jl:89-125 */
             if (tuned) n_prop += 1;
@@ -539,12 +595,14 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
         if (orc_kept(i - step0, burnin, thinning, len, &kk)) {
             if (samples)
                 for (int j = 0; j < d; ++j) samples[((size_t)kk * d + j) * C + c] = x[j];
-            if (grads && s->kind != ORC_RWM)
+            if (grads && s->kind != ORC_RWM && s->kind != ORC_RAM)
                 for (int j = 0; j < d; ++j) grads[((size_t)kk * d + j) * C + c] = g[j];
             if (acc_out) acc_out[(size_t)kk * C + c] = (uint8_t)acc;
         }
         /* adaptation, with the runner's burnin (`i <= runner.burnin`, MALA.jl:116, HMC.jl:293) */
-        if (s->kind == ORC_MALA && tuned && i <= burnin && (i % s->adapt_step) == 0) {
+        if (s->kind == ORC_RAM) {
+            orc_ram_update(st->ram_L + c, C, d, i, ram_ratio, s->rate, ram_nz, gp);
+        } else if (s->kind == ORC_MALA && tuned && i <= burnin && (i % s->adapt_step) == 0) {
             h = h * orc_tune_factor(n_acc, n_prop, s->target_rate);
             n_acc = 0;
             n_prop = 0;
@@ -571,7 +629,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
     }
     for (int j = 0; j < d; ++j) st->x[(size_t)j * C + c] = x[j];
     st->lp[c] = lp;
-    if (st->n_evals) st->n_evals[c] += (s->kind == ORC_RWM || s->kind == ORC_MALA) ? len : n_evals;
+    if (st->n_evals) st->n_evals[c] += (s->kind == ORC_RWM || s->kind == ORC_MALA || s->kind == ORC_RAM) ? len : n_evals;
     if (tuned || s->kind == ORC_HMCDA) st->t_step[c] = (s->kind == ORC_MALA) ? h : eps;
     if (s->kind == ORC_HMCDA) {
         st->t_bar[c] = eps_bar;
@@ -608,6 +666,11 @@ int64_t orc_init(const orc_model* m, const orc_sampler* s, int64_t C, orc_state*
         if (s->kind == ORC_MALA && tuned) st->t_step[c] = s->drift_step;
         if (s->kind == ORC_HMC && tuned) { st->t_step[c] = s->leap_step; st->t_leaps[c] = (int32_t)s->n_leaps; }
         if (s->kind == ORC_HMCDA) { st->t_step[c] = 1.0; st->t_bar[c] = 1.0; st->t_h[c] = 0.0; }
+        if (s->kind == ORC_RAM)                   /* S = diag(model.scale .* sampler.scale) (RAM.jl:51,55) */
+            for (int r = 0; r < d; ++r)
+                for (int q = 0; q <= r; ++q)
+                    st->ram_L[(size_t)(r * (r + 1) / 2 + q) * C + c] =
+                        q == r ? (m->scale ? m->scale[r] * s->scale : s->scale) : 0.0;
         if (tuned) { st->t_acc[c] = 0; st->t_prop[c] = 0; }
         if (st->n_evals) st->n_evals[c] = 0;
     }

@@ -37,7 +37,7 @@ class OSampler(ct.Structure):
 class OState(ct.Structure):
     _fields_ = [("x", D), ("lp", D), ("t_step", D), ("t_bar", D), ("t_h", D),
                 ("t_leaps", ct.POINTER(ct.c_int32)), ("t_acc", ct.POINTER(ct.c_int32)),
-                ("t_prop", ct.POINTER(ct.c_int32)), ("n_evals", ct.POINTER(ct.c_int64))]
+                ("t_prop", ct.POINTER(ct.c_int32)), ("n_evals", ct.POINTER(ct.c_int64)), ("ram_L", D)]
 
 
 _lib = None
@@ -137,9 +137,11 @@ class OracleChains:
         self.t_acc = np.zeros(C, dtype=np.int32)
         self.t_prop = np.zeros(C, dtype=np.int32)
         self.n_evals = np.zeros(C, dtype=np.int64)
+        # RAM jump factor, packed lower rows [d(d+1)/2][C]
+        self.ram_L = np.zeros((d * (d + 1) // 2 if sampler.kind == 5 else 1, C))
         self.st = OState(_d(self.x), _d(self.lp), _d(self.t_step), _d(self.t_bar), _d(self.t_h),
                          _i(self.t_leaps), _i(self.t_acc), _i(self.t_prop),
-                         self.n_evals.ctypes.data_as(ct.POINTER(ct.c_int64)))
+                         self.n_evals.ctypes.data_as(ct.POINTER(ct.c_int64)), _d(self.ram_L))
         bad = lib().orc_init(ct.byref(self.om.s), ct.byref(self.os), C, ct.byref(self.st), self.order)
         if bad:
             raise AssertionError("Initial values out of model support, try other values")
@@ -149,7 +151,7 @@ class OracleChains:
         d, C = self.om.size, self.C
         nk = len(runner.r)
         samples = np.full((nk, d, C), np.nan)
-        grads = np.full((nk, d, C), np.nan) if (want_grads and self.kind != 1) else None
+        grads = np.full((nk, d, C), np.nan) if (want_grads and self.kind not in (1, 5)) else None
         acc = np.zeros((nk, C), dtype=np.uint8)
         if nthreads is None:
             nthreads = min(8, os.cpu_count() or 1)

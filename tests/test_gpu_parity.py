@@ -389,3 +389,84 @@ def test_dist_dsl_sampler_parity(gpu, sname, dist, params, x0, d):
     oc = orc.OracleChains(m, sp(), nchains=130, seed=77 + d, order=order_for(d))
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
+
+
+# ------------------------------------------------------------------ RAM (RAM.jl)
+def _ram_model(mkind, d):
+    if mkind == "dist":
+        return mc.model(mc.DistDSL("Gamma", 2.5, 0.7), v=np.full(d, 1.2))
+    return _model(mkind, d)
+
+
+def _assert_ram_factor(task, oc, d):
+    S = task.ram_factor()
+    S_ref = mc.api.unpack_ram_factor(oc.ram_L, d)
+    assert np.array_equal(S.view(np.uint64), S_ref.view(np.uint64)), "jump factors not bit-identical"
+
+
+@pytest.mark.parametrize("mkind", ["iso", "normal", "abs", "dist"])
+@pytest.mark.parametrize("d", [1, 3, 7, 16, 17, 32])
+def test_ram_parity(gpu, mkind, d):
+    """lane-per-chain RAM: samples, accept bits, final state and every chain's jump factor S bit-identical
+    to the oracle (proposals out of the Gamma support -> -Inf -> downdates of S)."""
+    m = _ram_model(mkind, d)
+    C = 200
+    r = mc.SerialMC(steps=45, burnin=6, thinning=3)
+    task = (m * mc.RAM(0.7, 0.3) * r).batch(C, seed=4242 + d)
+    chain = mc.run(task)
+    oc = orc.OracleChains(m, mc.RAM(0.7, 0.3), nchains=C, seed=4242 + d)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert g_ref is None and chain._gradients is None
+    assert_parity(chain, s_ref, None, acc_ref, "ram")
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert task.evals == int(oc.n_evals.sum())
+    _assert_ram_factor(task, oc, d)
+
+
+@pytest.mark.parametrize("kind", ["logistic", "linear"])
+@pytest.mark.parametrize("d", [3, 10, 16, 17, 32])
+def test_glm_ram_parity(gpu, kind, d):
+    """RAM on the regression targets (examples/linear_regression.jl:28): the four lanes of a chain
+    rebuild S z, lane 0 stores the updated factor."""
+    m = _glm_model(kind, d)
+    C = 40
+    r = mc.SerialMC(steps=30, burnin=4, thinning=2)
+    task = (m * mc.RAM(1.0, 0.3) * r).batch(C, seed=31 + d)
+    chain = mc.run(task)
+    oc = orc.OracleChains(m, mc.RAM(1.0, 0.3), nchains=C, seed=31 + d)
+    s_ref, _, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, None, acc_ref, "ram")
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    _assert_ram_factor(task, oc, d)
+
+
+def test_ram_continue_spl_and_shards(gpu):
+    """S lives on the device between runs; steps per launch and chain offsets are invisible."""
+    d = 6
+    m = _model("normal", d)
+    r = mc.SerialMC(steps=30, burnin=5, thinning=5)
+    task = (m * mc.RAM() * r).batch(150, seed=8)
+    c1 = mc.run(task)
+    c2 = mc.run(c1)
+    oc = orc.OracleChains(m, mc.RAM(), nchains=150, seed=8)
+    s1, _, a1 = oc.run(r)
+    s2, _, a2 = oc.run(r)
+    assert_parity(c1, s1, None, a1, "ram")
+    assert_parity(c2, s2, None, a2, "ram")
+    _assert_ram_factor(task, oc, d)
+    b = mc.run((m * mc.RAM() * mc.SerialMC(steps=60, burnin=5, thinning=5)).batch(150, seed=8, steps_per_launch=7))
+    lo = mc.run((m * mc.RAM() * mc.SerialMC(steps=60, burnin=5, thinning=5)).batch(70, seed=8))
+    hi = mc.run((m * mc.RAM() * mc.SerialMC(steps=60, burnin=5, thinning=5)).batch(80, seed=8, chain_offset=70))
+    full = orc.OracleChains(m, mc.RAM(), nchains=150, seed=8)
+    s, _, _ = full.run(mc.SerialMC(steps=60, burnin=5, thinning=5))
+    assert np.array_equal(b._samples, s)
+    assert np.array_equal(np.concatenate([lo._samples, hi._samples], axis=2), s)
+
+
+def test_ram_limits(gpu):
+    m = _model("iso", 33)
+    with pytest.raises(mc.MCMCError, match="RAM is built for d <= 32"):
+        mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
+    m = _glm_model("linear", 40)
+    with pytest.raises(mc.MCMCError, match="RAM is built for d <= 32"):
+        mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
