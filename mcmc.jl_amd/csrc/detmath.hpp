@@ -33,8 +33,10 @@ __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        // three-input xor in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler's own
+        // combine leaves most of these as two v_xor_b32
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
         c1 = (uint32_t)p1;
         c3 = (uint32_t)p0;
         c0 = n0;
@@ -194,52 +196,46 @@ __device__ __forceinline__ double bm_log_u32(uint32_t w, const double (*tab)[4] 
     return hi + lo;
 }
 
-// det_sincos2pi(w 2^-32) with the quarter-turn reduction done in integers: q = floor(4u + 1/2) =
-// (w + 2^29) >> 30 and u - q/4 = ((w + 2^29) mod 2^30 - 2^29) 2^-32 -- the same q and r bit for bit.
-__device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, double& c_out) {
-    const uint32_t t = w + 0x20000000u;
-    const int qi = (int)(t >> 30);
-    const double r = (double)((int32_t)(t & 0x3fffffffu) - 0x20000000) * 0x1p-32;
+// sin, cos of 2 pi w 2^-32 (the Box-Muller angle), table-driven: the angle splits as k/256 + j 2^-32 turns
+// with k = (w + 2^23) >> 24 and |j| <= 2^23, so r = 2 pi j 2^-32 has |r| <= 2 pi 2^-9.  The row of k gives
+// (sin a, cos a) (scripts/gen_bm_log_table.py, full circle: no quadrant selects); sin r and cos r - 1 by
+// Taylor polynomials (truncation < 2^-66 relative); sin(a+r) = sa + (ca sin r + sa (cos r - 1)).
+static __device__ const double kBmSinCosTab[256][2] = {BM_SINCOS_TABLE_ROWS};
+
+__device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, double& c_out,
+                                                  const double (*sct)[2] = kBmSinCosTab) {
+    const uint32_t t = w + 0x800000u;
+    const uint32_t k = t >> 24;
+    const double r = (double)((int32_t)(t & 0xffffffu) - 0x800000) * 0x1.921fb54442d18p-30;
     const double r2 = r * r;
-    double S = -0x1.6fadb9f155744p-1;
-    S = __builtin_fma(S, r2, 0x1.e8f434d018d63p+1);
-    S = __builtin_fma(S, r2, -0x1.e3074fde8871fp+3);
-    S = __builtin_fma(S, r2, 0x1.50783487ee782p+5);
-    S = __builtin_fma(S, r2, -0x1.32d2cce62bd86p+6);
-    S = __builtin_fma(S, r2, 0x1.466bc6775aae2p+6);
-    S = __builtin_fma(S, r2, -0x1.4abbce625be53p+5);
-    S = __builtin_fma(S, r2, 0x1.921fb54442d18p+2);
-    double C = 0x1.20c62c2f2d7f5p-2;
-    C = __builtin_fma(C, r2, -0x1.b6e24f44b128fp+0);
-    C = __builtin_fma(C, r2, 0x1.f9d38a3763cc3p+2);
-    C = __builtin_fma(C, r2, -0x1.a6d1f2a204a8cp+4);
-    C = __builtin_fma(C, r2, 0x1.e1f506891babbp+5);
-    C = __builtin_fma(C, r2, -0x1.55d3c7e3cbffap+6);
-    C = __builtin_fma(C, r2, 0x1.03c1f081b5ac4p+6);
-    C = __builtin_fma(C, r2, -0x1.3bd3cc9be45dep+4);
-    C = __builtin_fma(C, r2, 1.0);
-    const double sn = r * S;
-    const double a = (qi & 1) ? C : sn;
-    const double b = (qi & 1) ? sn : C;
-    s_out = (qi & 2) ? -a : a;
-    c_out = (qi == 1 || qi == 2) ? -b : b;
+    double sp = __builtin_fma(r2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);   // -1/5040, 1/120
+    sp = __builtin_fma(r2, sp, -0x1.5555555555555p-3);                             // -1/6
+    const double sr = __builtin_fma(r * r2, sp, r);
+    double cp = __builtin_fma(r2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);   // -1/720, 1/24
+    cp = __builtin_fma(r2, cp, -0.5);
+    const double cm1 = r2 * cp;
+    typedef double f64x2_t __attribute__((ext_vector_type(2)));
+    const f64x2_t a = *reinterpret_cast<const f64x2_t*>(sct[k]);                   // (sin a, cos a)
+    s_out = a.x + __builtin_fma(a.y, sr, a.x * cm1);
+    c_out = a.y + __builtin_fma(-a.x, sr, a.y * cm1);
 }
 
 // Two Box-Muller pairs from one Philox block: radius sqrt(-2 log u1), u1 = (w.x + 1/2) 2^-32 in (0,1);
 // angle 2 pi u2, u2 = w.y 2^-32.
-// tab: the radius-log table, in global memory (default) or a kernel's LDS copy (stage_bm_log_table)
+// tab, sct: the radius-log and angle tables, in global memory (default) or a kernel's LDS copies
 __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3,
-                                         const double (*tab)[4] = kBmLogTab) {
+                                         const double (*tab)[4] = kBmLogTab,
+                                         const double (*sct)[2] = kBmSinCosTab) {
     {
         const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.x, tab));
         double s, c;
-        det_sincos2pi_u32(w.y, s, c);
+        det_sincos2pi_u32(w.y, s, c, sct);
         z0 = rad * c; z1 = rad * s;
     }
     {
         const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.z, tab));
         double s, c;
-        det_sincos2pi_u32(w.w, s, c);
+        det_sincos2pi_u32(w.w, s, c, sct);
         z2 = rad * c; z3 = rad * s;
     }
 }

@@ -43,16 +43,21 @@ struct LaneChain {
     int64_t c;        // local chain index
     bool live;        // c < C
     int d;
-    const double (*tab)[4];   // LDS copy of the Box-Muller log table: per-lane row gathers from LDS,
-                              // not from the vector L1 (every block thread calls the constructor)
+    const double (*tab)[4];   // LDS copies of the Box-Muller log and angle tables: per-lane row gathers
+    const double (*sct)[2];   // from LDS, not from the vector L1 (every block thread calls the constructor)
     __device__ LaneChain(const StepArgs& s) {
         c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
         live = c < s.C;
         d = s.d;
         __shared__ __attribute__((aligned(16))) double lds_tab[128][4];
-        for (int i = threadIdx.x; i < 128 * 4; i += kBlock) lds_tab[i >> 2][i & 3] = kBmLogTab[i >> 2][i & 3];
+        __shared__ __attribute__((aligned(16))) double lds_sct[256][2];
+        for (int i = threadIdx.x; i < 128 * 4; i += kBlock) {
+            lds_tab[i >> 2][i & 3] = kBmLogTab[i >> 2][i & 3];
+            lds_sct[i >> 1][i & 1] = kBmSinCosTab[i >> 1][i & 1];
+        }
         __syncthreads();
         tab = lds_tab;
+        sct = lds_sct;
     }
     __device__ __forceinline__ int coord(int k) const { return k; }
     // blocks 0..NB-2 are always full (NB = ceil(d/4)); only the last block's coordinates are tested
@@ -196,6 +201,7 @@ struct WaveChain {
         if (s.n_evals != nullptr && live && lane == 0) atomicAdd(s.n_evals, (unsigned long long)n);
     }
     const double (*tab)[4] = kBmLogTab;
+    const double (*sct)[2] = kBmSinCosTab;
     __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
         if (live && lane == 0 && acc && s.acc_bits != nullptr)
             atomicOr((unsigned long long*)&s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)(c >> 6)],
@@ -210,7 +216,7 @@ __device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32
 #pragma unroll
     for (int b = 0; b < P::NB; ++b) {
         const u32x4 w = rs.block(chain, step, p.block(b), TAG_NORMAL);
-        normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3], p.tab);
+        normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3], p.tab, p.sct);
     }
 }
 

@@ -16,6 +16,7 @@
  *                       path, explicit fma in the polynomial
  *   det_exp ........... Cody-Waite reduction + degree-13 Taylor (fma Horner)
  *   det_sincos2pi ..... exact quarter-turn reduction + Taylor polynomials in r
+ *   Box-Muller angle .. 256-row sin/cos table + short Taylor polynomials (orc_sincos2pi_u32)
  *   Box-Muller ........ normals from 32-bit uniforms, 4 normals per Philox block
  *
  * Compile with -ffp-contract=off: every fused multiply-add is an explicit fma();
@@ -218,12 +219,35 @@ static inline double orc_bm_log_u32(uint32_t w) {
     return hi + lo;
 }
 
+/* ------------------------------------------------------- Box-Muller angle */
+/* sin, cos of 2 pi w 2^-32: angle = k/256 + j 2^-32 turns, k = (w + 2^23) >> 24, |j| <= 2^23; the row of k
+   holds RN(sin, cos of 2 pi k/256) (scripts/gen_bm_log_table.py); r = 2 pi j 2^-32 (|r| <= 2 pi 2^-9),
+   sin r and cos r - 1 by Taylor (truncation < 2^-66 relative), then the angle-addition formula.  The
+   device twin is det_sincos2pi_u32 (csrc/detmath.hpp). */
+static const double orc_bm_sincos_tab[256][2] = {BM_SINCOS_TABLE_ROWS};
+
+static inline void orc_sincos2pi_u32(uint32_t w, double* s_out, double* c_out) {
+    uint32_t t = w + 0x800000u;
+    uint32_t k = t >> 24;
+    double r = (double)((int32_t)(t & 0xffffffu) - 0x800000) * 0x1.921fb54442d18p-30;
+    double r2 = r * r;
+    double sp = fma(r2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);
+    sp = fma(r2, sp, -0x1.5555555555555p-3);
+    double sr = fma(r * r2, sp, r);
+    double cp = fma(r2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);
+    cp = fma(r2, cp, -0.5);
+    double cm1 = r2 * cp;
+    double sa = orc_bm_sincos_tab[k][0], ca = orc_bm_sincos_tab[k][1];
+    *s_out = sa + fma(ca, sr, sa * cm1);
+    *c_out = ca + fma(-sa, sr, ca * cm1);
+}
+
 /* Four standard normals from one Philox block (two Box-Muller pairs). */
 static inline void orc_normals4(const uint32_t w[4], double z[4]) {
     for (int p = 0; p < 2; ++p) {
         double rad = sqrt(-2.0 * orc_bm_log_u32(w[2 * p]));
         double s, c;
-        orc_sincos2pi(orc_uniform32(w[2 * p + 1]), &s, &c);
+        orc_sincos2pi_u32(w[2 * p + 1], &s, &c);
         z[2 * p] = rad * c;
         z[2 * p + 1] = rad * s;
     }

@@ -94,6 +94,20 @@ def test_det_sincos2pi_accuracy():
     assert np.allclose(q, [0, 1, 0, -1], atol=1e-16)
 
 
+def test_sincos2pi_u32_accuracy():
+    """Box-Muller angle sin/cos(2 pi w 2^-32), table-driven: within 4.5e-16 (2 ulp of 1) of a long-double reference,
+    exact at the table nodes, including the wrap at w -> 2^32."""
+    rng = np.random.default_rng(12)
+    w = np.concatenate([np.floor(rng.uniform(0, 2**32, 300000)), np.arange(0, 3000), 2.0**32 - 1 - np.arange(0, 3000),
+                        (np.arange(-40, 40) + 2.0**23 * np.arange(1, 512, 2)[:, None]).ravel() % 2**32])
+    s, c = orc.detmath(10, w), orc.detmath(11, w)
+    a = 2 * np.pi * (w.astype(np.longdouble) * np.longdouble(2.0)**-32)
+    assert np.abs(s - np.sin(a)).max() < 4.5e-16
+    assert np.abs(c - np.cos(a)).max() < 4.5e-16
+    k = np.arange(0, 256) * 2.0**24
+    np.testing.assert_array_equal(orc.detmath(10, k[[0, 64, 128, 192]]), [0.0, 1.0, 0.0, -1.0])
+
+
 def test_round_ties_away_from_zero():
     x = np.array([0.5, 1.5, 2.5, -0.5, -2.5, 2.4999999999, 0.49999999999999994, 3.0])
     assert list(orc.detmath(7, x)) == [1, 2, 3, -1, -3, 2, 0, 3]      # Julia 0.2 round (HMCDA.jl:104)
