@@ -132,6 +132,20 @@ def kernel_name(cfg, d, sampler):
     return f"{'lpc' if d <= 32 else 'wpc'}_{sampler}"
 
 
+def measured_traffic(wkey):
+    """HBM bytes per launch of the step kernel for this workload: 2 x FETCH_SIZE + WRITE_SIZE of the timed
+    dispatch in a committed rocprofv3 run of the same bench command (MI355X_MICROARCH.md §HBM correction),
+    or None when no profile of this exact workload is committed."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    e = json.load(open(p)).get(wkey)
+    if e is None:
+        return None
+    return {"bytes_per_launch": e["traffic_bytes"], "read_bytes": e["read_bytes"], "write_bytes": e["write_bytes"],
+            "source": e["source"], "unit": "B"}
+
+
 def cpu_baseline(model, sampler, seconds, C=4096):
     """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -165,10 +179,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     import torch            # first: libmcmc_hip.so then binds to the HIP runtime torch already loaded
+    # MCMC_BENCH_BACKEND=gloo: rehearse the multi-rank path on a 1-GPU box (ranks share cuda:0, host-side
+    # reductions); the driver's N-GPU runs use the default, RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("MCMC_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            local = local % max(1, torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    red_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
     import mcmchip as mc
     from mcmchip import _lib
 
@@ -222,7 +244,7 @@ def main():
     kernel_ms = out.kernel_ms
     evals = task.evals - ev0
     if dist is not None:
-        t = torch.tensor([T, kernel_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([T, kernel_ms], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         T, kernel_ms = float(t[0]), float(t[1])
     total_chains = C * world
@@ -240,6 +262,7 @@ def main():
         torch.cuda.synchronize(dev)
         ess_s = time.perf_counter() - te
         if dist is not None:
+            ess_min_sum = ess_min_sum.to(red_dev)
             dist.all_reduce(ess_min_sum, op=dist.ReduceOp.SUM)
         ess_line = {"ess_per_sec": float(ess_min_sum) / T, "vtype": "imse", "kept_per_chain": nkept,
                     "sum_min_ess": float(ess_min_sum), "ess_compute_s": ess_s,
@@ -248,6 +271,11 @@ def main():
 
     spl = args.spl if args.spl >= 0 else 0
     launches = 1 if spl == 0 else -(-K // spl)
+    # per-GPU workload key: the PMC traffic of a committed rocprofv3 run of this same workload
+    # (profiles/traffic.json, written by scripts/summarize_prof.py) fills roofline.traffic
+    wkey = f"{args.config}|d={d}|chains={C}|{args.sampler}|steps={K}|thinning={args.thinning}|spl={spl}"
+    tdet = measured_traffic(wkey)
+    traffic = tdet["bytes_per_launch"] if tdet else None
     avg_launch_s = kernel_ms * 1e-3 / launches          # HIP events around the launches, on their stream
     kname = kernel_name(cfg0, d, args.sampler)
     if cfg0["model"] == "iso":
@@ -256,7 +284,7 @@ def main():
         achieved = nbytes / launches / avg_launch_s / 1e9
         moved = (launches * C * (16 * d + 16) + C * nkept * per_kept) / launches / avg_launch_s / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname, "launches": launches,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname, "launches": launches,
                 "avg_launch_ms": avg_launch_s * 1e3,
                 "algorithmic_bytes_per_launch": nbytes / launches,
                 "units_per_launch": C * K / launches,
@@ -270,7 +298,7 @@ def main():
         flops = flop_per_eval * evals
         achieved = flops / launches / avg_launch_s / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": None, "kernel": kname, "launches": launches,
+                "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname, "launches": launches,
                 "avg_launch_ms": avg_launch_s * 1e3, "flop_per_eval": flop_per_eval,
                 "evals_per_launch": evals / launches,
                 "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
@@ -295,7 +323,7 @@ def main():
                         f"thinning={args.thinning}), {C} chains/GPU, {type(sampler).__name__}",
             "d": d, "chains_per_gpu": C, "global_chains": total_chains, "sampler": args.sampler,
             "burnin": burnin, "thinning": args.thinning, "kept_per_chain": nkept,
-            "steps_per_launch": spl, "evals": evals,
+            "steps_per_launch": spl, "evals": evals, "key": wkey,
             "parallelism": f"chains sharded over {world} GPU(s), no collective in the step loop",
         },
         "roofline": roof,

@@ -220,6 +220,24 @@ __device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, dou
     c_out = a.y + __builtin_fma(-a.x, sr, a.y * cm1);
 }
 
+// IEEE sqrt of a positive normal finite x: the hardware rsq estimate refined by the same Newton/fma
+// sequence hipcc emits for __builtin_sqrt (Goldschmidt, then two residual corrections), without its
+// guards -- the 2^256 pre-scale of x < 2^-767 and the 0/inf class selects -- which never fire for the
+// Box-Muller radius argument -2 log u in [2.3e-10, 46].  Correctly rounded, so the oracle's sqrt() is its
+// twin (tests/test_gpu_parity.py checks it bit for bit over the normal range).
+__device__ __forceinline__ double sqrt_pos_normal(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = 0.5 * y;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double e = __builtin_fma(-g, g, x);
+    g = __builtin_fma(e, h, g);
+    e = __builtin_fma(-g, g, x);
+    return __builtin_fma(e, h, g);
+}
+
 // Two Box-Muller pairs from one Philox block: radius sqrt(-2 log u1), u1 = (w.x + 1/2) 2^-32 in (0,1);
 // angle 2 pi u2, u2 = w.y 2^-32.
 // tab, sct: the radius-log and angle tables, in global memory (default) or a kernel's LDS copies
@@ -227,13 +245,13 @@ __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1,
                                          const double (*tab)[4] = kBmLogTab,
                                          const double (*sct)[2] = kBmSinCosTab) {
     {
-        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.x, tab));
+        const double rad = sqrt_pos_normal(-2.0 * bm_log_u32(w.x, tab));
         double s, c;
         det_sincos2pi_u32(w.y, s, c, sct);
         z0 = rad * c; z1 = rad * s;
     }
     {
-        const double rad = __builtin_sqrt(-2.0 * bm_log_u32(w.z, tab));
+        const double rad = sqrt_pos_normal(-2.0 * bm_log_u32(w.z, tab));
         double s, c;
         det_sincos2pi_u32(w.w, s, c, sct);
         z2 = rad * c; z3 = rad * s;

@@ -78,6 +78,7 @@ __global__ void k_detmath(int op, int64_t n, const double* x, const double* y, d
         case 9: r = bm_log_u32((uint32_t)(uint64_t)a); break;
         case 10: { double s, c; det_sincos2pi_u32((uint32_t)(uint64_t)a, s, c); r = s; } break;
         case 11: { double s, c; det_sincos2pi_u32((uint32_t)(uint64_t)a, s, c); r = c; } break;
+        case 12: r = sqrt_pos_normal(a); break;
         default: r = 0.0;
     }
     out[i] = r;

@@ -738,6 +738,7 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
             case 9: r = orc_bm_log_u32((uint32_t)(uint64_t)a); break;
             case 10: orc_sincos2pi_u32((uint32_t)(uint64_t)a, &sn, &cs); r = sn; break;
             case 11: orc_sincos2pi_u32((uint32_t)(uint64_t)a, &sn, &cs); r = cs; break;
+            case 12: r = sqrt(a); break;     /* device: sqrt_pos_normal (guard-free IEEE sequence) */
             case 8: {
                 uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
                 uint32_t key[2] = {0u, 0u}, w[4];

@@ -52,7 +52,7 @@ def _dev_math(op, x, y=None):
 
 @pytest.mark.parametrize("op,name", [(0, "log"), (1, "exp"), (2, "sin2pi"), (3, "cos2pi"), (4, "sqrt"),
                                      (5, "div"), (7, "round"), (9, "bm_log_u32"), (10, "sin2pi_u32"),
-                                     (11, "cos2pi_u32")])
+                                     (11, "cos2pi_u32"), (12, "sqrt_pos_normal")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -63,6 +63,11 @@ def test_device_detmath_bitwise(gpu, op, name):
         x = np.floor(rng.uniform(0, 2**32, 200000)) * 2.0**-32
     elif op == 4:
         x = np.exp(rng.uniform(-700, 700, 200000))
+    elif op == 12:               # positive normals; dense over the Box-Muller radius argument [2.3e-10, 46]
+        x = np.concatenate([np.exp(rng.uniform(-700, 700, 200000)), rng.uniform(2.3e-10, 46.0, 200000),
+                            -2.0 * np.log((np.arange(0, 4000) + 0.5) * 2.0**-32),
+                            -2.0 * np.log((2.0**32 - 0.5 - np.arange(0, 4000)) * 2.0**-32),
+                            np.nextafter(np.arange(1.0, 47.0) ** 2, 0), np.arange(1.0, 47.0) ** 2])
     elif op in (9, 10, 11):      # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
         x = np.concatenate([np.floor(rng.uniform(0, 2**32, 200000)), np.arange(0, 2000),
                             2.0**32 - 1 - np.arange(0, 2000), (np.arange(-40, 40) + 2**29 * np.arange(1, 8)[:, None]
