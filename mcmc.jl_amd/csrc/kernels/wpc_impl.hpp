@@ -9,29 +9,37 @@ namespace mcmc {
 
 constexpr int kChainsPerBlock = kBlock / 64;
 
-template <int NB, class M>
-__global__ __launch_bounds__(kBlock) void wpc_rwm(KernelArgs a) { rwm_body<WaveChain<NB>, M>(a); }
-template <int NB, class M>
-__global__ __launch_bounds__(kBlock) void wpc_mala(KernelArgs a) { mala_body<WaveChain<NB>, M>(a); }
-template <int NB, class M, bool DA>
-__global__ __launch_bounds__(kBlock) void wpc_hmc(KernelArgs a) { hmc_body<WaveChain<NB>, M, DA>(a); }
+// F: d == 256 NB (WaveChain FULL)
+template <int NB, bool F, class M>
+__global__ __launch_bounds__(kBlock) void wpc_rwm(KernelArgs a) { rwm_body<WaveChain<NB, F>, M>(a); }
+template <int NB, bool F, class M>
+__global__ __launch_bounds__(kBlock) void wpc_mala(KernelArgs a) { mala_body<WaveChain<NB, F>, M>(a); }
+template <int NB, bool F, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void wpc_hmc(KernelArgs a) { hmc_body<WaveChain<NB, F>, M, DA>(a); }
 template <int NB, class M>
 __global__ __launch_bounds__(kBlock) void wpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {
     eval_body<WaveChain<NB>, M>(a, xin, lp, g, check);
 }
 
-template <int NB, class M>
+template <int NB, bool F, class M>
 static hipError_t wpc_launch_model(const KernelArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
     switch (a.sa.kind) {
-        case SK_RWM: wpc_rwm<NB, M><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_MALA: wpc_mala<NB, M><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_HMC: wpc_hmc<NB, M, false><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_HMCDA: wpc_hmc<NB, M, true><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_RWM: wpc_rwm<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_MALA: wpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMC: wpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_HMCDA: wpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+// SPEC: instantiate the FULL (d == 256 NB) variants too -- for the models the benchmarks run
+template <int NB, class M, bool SPEC>
+static hipError_t wpc_launch_nb(const KernelArgs& a, hipStream_t st) {
+    if (SPEC && a.s.d == 256 * NB) return wpc_launch_model<NB, SPEC, M>(a, st);
+    return wpc_launch_model<NB, false, M>(a, st);
 }
 
 // G = Philox blocks per lane: d <= 256 G, 4 (l + 64k) + e < d
@@ -43,13 +51,13 @@ static inline int wpc_nb_for(int d) {
     return 0;
 }
 
-template <class M>
+template <class M, bool SPEC>
 static hipError_t wpc_step(const KernelArgs& a, hipStream_t st) {
     switch (wpc_nb_for(a.s.d)) {
-        case 1: return wpc_launch_model<1, M>(a, st);
-        case 2: return wpc_launch_model<2, M>(a, st);
-        case 4: return wpc_launch_model<4, M>(a, st);
-        case 8: return wpc_launch_model<8, M>(a, st);
+        case 1: return wpc_launch_nb<1, M, SPEC>(a, st);
+        case 2: return wpc_launch_nb<2, M, SPEC>(a, st);
+        case 4: return wpc_launch_nb<4, M, SPEC>(a, st);
+        case 8: return wpc_launch_nb<8, M, SPEC>(a, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -70,9 +78,9 @@ static hipError_t wpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
 
 }  // namespace mcmc
 
-#define WPC_UNIT(name, Model)                                                                            \
+#define WPC_UNIT(name, Model, SPEC)                                                                      \
     hipError_t mcmc_wpc_step_##name(const mcmc::KernelArgs& a, hipStream_t st) {                         \
-        return mcmc::wpc_step<mcmc::Model>(a, st);                                                      \
+        return mcmc::wpc_step<mcmc::Model, SPEC>(a, st);                                                \
     }                                                                                                    \
     hipError_t mcmc_wpc_eval_##name(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, \
                                     int check, hipStream_t st) {                                         \

@@ -1,3 +1,3 @@
 // wpc_normal.hip -- wave-per-chain kernels of v ~ Normal(mu, sigma)
 #include "wpc_impl.hpp"
-WPC_UNIT(normal, NormalDSL)
+WPC_UNIT(normal, NormalDSL, false)

@@ -131,7 +131,9 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-template <int G>
+// FULL: d == 256 G, every lane coordinate is a real one -- no per-coordinate validity masks (with a
+// runtime d they are 4 G lane masks live across the step loop, which spill the scalar file)
+template <int G, bool FULL = false>
 struct WaveChain {
     static constexpr int NB = G;
     static constexpr int NC = 4 * G;
@@ -140,15 +142,26 @@ struct WaveChain {
     int d;
     int lane;
     int64_t ldr;      // row stride of chain-major state (multiple of 4)
+    const double (*tab)[4];   // LDS copies of the Box-Muller tables (as LaneChain)
+    const double (*sct)[2];
     __device__ WaveChain(const StepArgs& s) {
         c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
         live = c < s.C;
         d = s.d;
         lane = threadIdx.x & 63;
         ldr = s.ld;
+        __shared__ __attribute__((aligned(16))) double lds_tab[128][4];
+        __shared__ __attribute__((aligned(16))) double lds_sct[256][2];
+        for (int i = threadIdx.x; i < 128 * 4; i += kBlock) {
+            lds_tab[i >> 2][i & 3] = kBmLogTab[i >> 2][i & 3];
+            lds_sct[i >> 1][i & 1] = kBmSinCosTab[i >> 1][i & 1];
+        }
+        __syncthreads();
+        tab = lds_tab;
+        sct = lds_sct;
     }
     __device__ __forceinline__ int coord(int k) const { return 4 * (lane + 64 * (k >> 2)) + (k & 3); }
-    __device__ __forceinline__ bool valid(int k) const { return coord(k) < d; }
+    __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + 64 * b); }
     __device__ __forceinline__ double reduce(double v) const { return wave_sum(v); }
     __device__ __forceinline__ void load(const double* x, int64_t /*ld*/, double (&v)[NC]) const {
@@ -156,7 +169,7 @@ struct WaveChain {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int j0 = 4 * (lane + 64 * g);
-            if (j0 < d) {
+            if (FULL || j0 < d) {
                 const double4 q = *reinterpret_cast<const double4*>(row + j0);
                 v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
             } else {
@@ -173,7 +186,7 @@ struct WaveChain {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int j0 = 4 * (lane + 64 * g);
-            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
+            if (FULL || j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
                                                                                v[4 * g + 3]);
         }
     }
@@ -193,15 +206,13 @@ struct WaveChain {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int j0 = 4 * (lane + 64 * g);
-            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
+            if (FULL || j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
                                                                                v[4 * g + 3]);
         }
     }
     __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
         if (s.n_evals != nullptr && live && lane == 0) atomicAdd(s.n_evals, (unsigned long long)n);
     }
-    const double (*tab)[4] = kBmLogTab;
-    const double (*sct)[2] = kBmSinCosTab;
     __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
         if (live && lane == 0 && acc && s.acc_bits != nullptr)
             atomicOr((unsigned long long*)&s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)(c >> 6)],
@@ -376,25 +387,42 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
 
 // ------------------------------------------------------------------ HMC / HMCDA
 // nl leapfrogs from (x, m) (HMC.jl:219-228); the start point is in support.
+// Two restructurings, both bitwise neutral:
+//  * the half kick (0.5 g) eps at a point is computed once and used by the closing half kick of one
+//    leapfrog and the opening one of the next (the same x, the same oos flag) -- when the chain's
+//    coordinates are few enough (NC <= 16) for the carried kicks to stay in registers;
+//  * a model without the LLAcc rule (a function model) never goes out of support, so only the last
+//    leapfrog's log-target is used: it is evaluated once, after the loop.
 template <class P, class M>
 __device__ __forceinline__ double trajectory(const P& p, const M& model, double eps, int64_t nl, double (&x)[P::NC],
                                              double (&m)[P::NC]) {
+    constexpr bool kCarry = P::NC <= 16;
     bool oos = false;
     double lpl = 0.0;
+    double kick[kCarry ? P::NC : 1];
+    if constexpr (kCarry) {
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) kick[k] = (0.5 * model.grad(x[k])) * eps;
+    }
     for (int64_t l = 0; l < nl; ++l) {
 #pragma unroll
         for (int k = 0; k < P::NC; ++k) {
-            const double g = oos ? 0.0 : model.grad(x[k]);
-            m[k] = m[k] + (0.5 * g) * eps;                      // n.m += 0.5*n.grad*ve
+            double a;
+            if constexpr (kCarry) a = kick[k];
+            else a = (0.5 * (oos ? 0.0 : model.grad(x[k]))) * eps;
+            m[k] = m[k] + a;                                    // n.m += 0.5*n.grad*ve
             x[k] = x[k] + eps * m[k];                           // n.pars += ve * n.m
         }
-        lpl = eval_lp(p, model, x, oos);                        // calc!(n, ll)
+        if (M::kLLAcc) lpl = eval_lp(p, model, x, oos);         // calc!(n, ll)
 #pragma unroll
         for (int k = 0; k < P::NC; ++k) {
             const double g = oos ? 0.0 : model.grad(x[k]);
-            m[k] = m[k] + (0.5 * g) * eps;
+            const double a = (0.5 * g) * eps;
+            if constexpr (kCarry) kick[k] = a;
+            m[k] = m[k] + a;
         }
     }
+    if (!M::kLLAcc && nl > 0) lpl = eval_lp(p, model, x, oos);
     return lpl;
 }
 
