@@ -124,10 +124,10 @@ def hbm_bytes_per_unit(d, sampler):
 def kernel_name(cfg, d, sampler):
     if cfg["model"] != "iso":
         nm = 1
-        while d <= 64 and 16 * nm < d:
+        while d <= 128 and 16 * nm < d:
             nm *= 2
-        nw = 1 if d <= 64 else next(w for w in (2, 4, 8) if 64 * w >= d)
-        nm = nm if d <= 64 else 4
+        nw = 1 if d <= 128 else next(w for w in (4, 8) if 64 * w >= d)
+        nm = nm if d <= 128 else 4
         return f"glm_{'hmc' if sampler.startswith('hmc') else sampler}<{nm},{nw}{',DA' if sampler == 'hmcda' else ''}>"
     return f"{'lpc' if d <= 32 else 'wpc'}_{sampler}"
 

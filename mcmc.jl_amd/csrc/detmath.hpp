@@ -75,7 +75,10 @@ __device__ __forceinline__ double det_log(double x) {
     uint64_t bx = d2bits(x);
     int k = 0;
     const bool sub = bx < 0x0010000000000000ull;            // zero or subnormal (or negative: handled below)
-    if (sub && x > 0.0) { x = x * 0x1p54; k = -54; bx = d2bits(x); }
+    const bool scl = sub && x > 0.0;                         // subnormal: scale by 2^54 (selects, no branch)
+    x = scl ? x * 0x1p54 : x;
+    k = scl ? -54 : 0;
+    bx = d2bits(x);
     uint32_t hx = (uint32_t)(bx >> 32);
     k += (int)((hx >> 20) & 0x7ff) - 1023;
     hx &= 0x000fffffu;

@@ -81,7 +81,11 @@ __device__ __forceinline__ int own_coord(const GlmPos& p, int slot) {
     return p.base + 16 * (slot >> 2) + 4 * p.q + (slot & 3);
 }
 
-// LDS carve-up (doubles): X tiles [2][16][stride] | Y tiles [2][16] | eta partials [8 waves][64][4] |
+// X/Y tile buffers in LDS: the d-sliced evaluation double-buffers, the single-slice one (glm_eval1) keeps
+// three (tile t for G, t+1 for eta, t+2 being written)
+__host__ __device__ constexpr int glm_xbufs(int nw) { return nw == 1 ? 3 : 2; }
+
+// LDS carve-up (doubles): X tiles [3][16][stride] | Y tiles [3][16] | eta partials [8 waves][64][4] |
 // chain scalars [8 waves][16] | residual weights [4 tiles][4][64] | int scratch
 struct GlmLds {
     double* X;
@@ -95,8 +99,8 @@ struct GlmLds {
 __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     GlmLds L;
     L.X = smem;
-    L.Y = L.X + 2 * 16 * a.g.lds_stride;             // X: two tile buffers
-    L.part = L.Y + 2 * 16;
+    L.Y = L.X + glm_xbufs(a.g.nw) * 16 * a.g.lds_stride;     // X tile buffers
+    L.part = L.Y + glm_xbufs(a.g.nw) * 16;
     L.scal = L.part + kGlmMaxWaves * 64 * 4;
     L.rbuf = L.scal + kGlmMaxWaves * 16;
     L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
@@ -104,7 +108,7 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
 }
 
 size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(2 * 16 * g.lds_stride + 2 * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4 * 4 * 64 + 4) * 8;
+    return (size_t)(glm_xbufs(g.nw) * 16 * g.lds_stride + glm_xbufs(g.nw) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4 * 4 * 64 + 4) * 8;
 }
 
 // sum of a per-chain quantity held as 4 quarter partials per wave and NW slice partials:
@@ -134,12 +138,216 @@ __device__ __forceinline__ int64_t glm_max(const GlmLds& L, int64_t v, bool live
     return r;
 }
 
+// The end of an evaluation: likelihood partials combined (quarters, then slices left to right), the
+// prior vars ~ Normal(0, sp) over own coordinates, the LLAcc rule, and the prior's gradient added to G.
+template <int NM, int NW, bool GRAD>
+__device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
+                                          const double (&x)[(4 * NM)], f64x4 (&G)[NM], double lik_part, bool& oos) {
+    const ModelArgs& M = a.m;
+    const int d = M.d;
+    const double lik = glm_sum(a, p, L, lik_part);
+    // prior vars ~ Normal(0, sp) over own coordinates
+    const double sp = M.prior_sigma, s2p = sp * sp, logsp = det_log(sp);
+    double pp = 0.0;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot) {
+        const int k = own_coord(p, slot);
+        if (true && k < d) {
+            const double z = (x[slot] - 0.0) / sp;
+            pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
+        }
+    }
+    const double prior = glm_sum(a, p, L, pp);
+    double acc = 0.0 + prior;                                           // LLAcc(0.) + ...
+    bool bad = !(acc - acc == 0.0);
+    acc = acc + lik;
+    bad = bad || !(acc - acc == 0.0);
+    oos = bad;
+    if (bad) acc = -__builtin_inf();
+    if (GRAD) {
+#pragma unroll
+        for (int slot = 0; slot < (4 * NM); ++slot)
+            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - x[slot]) / s2p + G[slot >> 2][slot & 3];
+    }
+    return acc;
+}
+
+// Single-slice evaluation (NW = 1: the wave holds all d_pad coordinates of its 16 chains), software
+// pipelined over the 16-observation tiles with three LDS tile buffers:
+//     iteration t:  eta_{t+1} = X_{t+1} beta   (MFMA chain, buffer (t+1) % 3)
+//                   elementwise on eta_t        (VALU, independent of the chain above: the two interleave)
+//                   G += X_t^T r_t              (MFMA, buffer t % 3)
+//                   tile t+2 -> buffer (t+2) % 3 (its last readers finished before the previous barrier)
+//                   one barrier
+// The arithmetic is glm_eval's, operation for operation (eta chains over (m, e, q); G chains over
+// observations; a lane's likelihood terms in (t, r) order), so the oracle's orc_glm_eval restates both.
+template <int NM, bool GRAD, bool LOGI>
+__device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
+                                                const double (&x)[(4 * NM)], f64x4 (&G)[NM]) {
+    const ModelArgs& M = a.m;
+    const GlmShape& g = a.g;
+    const int S = g.lds_stride;
+    const double sgn = M.link_sign;
+    const double sn = M.noise_sigma, s2n = sn * sn;
+    const double logsn = LOGI ? 0.0 : det_log(sn);
+    const double isn = 1.0 / sn, is2n = 1.0 / s2n;
+    double lik_part = 0.0;
+    const int64_t ntiles = g.n_pad / 16;
+    constexpr int kBlk = glm_block<1>();
+    constexpr int kHalf = 16 * 8 * NM;                        // f64x2 per tile (d_pad = 16 NM)
+    constexpr int kPer = (kHalf + kBlk - 1) / kBlk;
+    constexpr int kLgHalfrow = __builtin_ctz(8 * NM);
+    const int XS = 16 * S;
+    f64x2 buf[kPer];
+    double ytile = 0.0;
+    auto load_tile = [&](int64_t tt) {
+        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * 16 * g.d_pad);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = threadIdx.x + kBlk * j;
+            buf[j] = src[i < kHalf ? i : 0];
+        }
+        ytile = (threadIdx.x < 16) ? M.Y[tt * 16 + threadIdx.x] : 0.0;
+    };
+    auto store_tile = [&](int b) {
+        double* Xb = L.X + b * XS;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = threadIdx.x + kBlk * j;
+            if (i < kHalf) {
+                const int row = i >> kLgHalfrow, col = 2 * (i & ((1 << kLgHalfrow) - 1));
+                *reinterpret_cast<f64x2*>(&Xb[row * S + col]) = buf[j];
+            }
+        }
+        if (threadIdx.x < 16) L.Y[b * 16 + threadIdx.x] = ytile;
+    };
+    // eta of the tile in buffer b: k-slice kk = 4m + e, row q <-> coordinate 16m + 4q + e
+    auto eta_of = [&](int b) {
+        f64x4 e = f64x4{0.0, 0.0, 0.0, 0.0};
+        const double* xrow = L.X + b * XS + p.cl * S + 4 * p.q;
+#pragma unroll
+        for (int slot = 0; slot < (4 * NM); ++slot)
+            e = __builtin_amdgcn_mfma_f64_16x16x4f64(xrow[16 * (slot >> 2) + (slot & 3)], x[slot], e, 0, 0, 0);
+        return e;
+    };
+    load_tile(0);
+    store_tile(0);
+    if (ntiles > 1) {
+        load_tile(1);
+        store_tile(1);
+    }
+    if (GRAD) {
+#pragma unroll
+        for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    __syncthreads();
+    f64x4 eta = eta_of(0);
+    int b = 0;                                                // buffer of tile t
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const bool more = t + 2 < ntiles;
+        if (more) load_tile(t + 2);
+        const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;
+        // eta_{t+1} (buffer b1; garbage past the last tile, unused) in four chunks of NM k-slices, each
+        // beside one observation row's elementwise work on eta_t: the chunk's MFMAs and the row's VALU
+        // chain are independent and interleave (scheduling groups: one MFMA, then up to kVPM VALU).  A
+        // chunk's LDS operands are read one chunk ahead, so no MFMA waits on its ds_read.
+        constexpr int kVPM = LOGI ? (NM >= 8 ? 12 : 24) : 4;
+        f64x4 eta_next = f64x4{0.0, 0.0, 0.0, 0.0};
+        const double* xrow1 = L.X + b1 * XS + p.cl * S + 4 * p.q;
+        const double* LY = L.Y + b * 16;
+        double rv[4];
+        double av[NM];
+#pragma unroll
+        for (int sl = 0; sl < NM; ++sl) av[sl] = xrow1[16 * (sl >> 2) + (sl & 3)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double an[NM];
+            if (r < 3) {
+#pragma unroll
+                for (int sl = 0; sl < NM; ++sl) {
+                    const int slot = (r + 1) * NM + sl;
+                    an[sl] = xrow1[16 * (slot >> 2) + (slot & 3)];
+                }
+            }
+            const double y = LY[p.q + 4 * r];
+#pragma unroll
+            for (int sl = 0; sl < NM; ++sl)
+                eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[sl], x[r * NM + sl], eta_next, 0, 0, 0);
+            const double e = eta[r];
+            const int64_t obs = t * 16 + p.q + 4 * r;
+            double term, w;
+            if (LOGI) {
+                const double tt = det_exp(-(sgn * e));                  // prob = 1/(1+exp(-X*vars))
+                const double pr = 1.0 / (1.0 + tt);
+                term = det_log((y >= 0.5) ? pr : 1.0 - pr);             // Y ~ Bernoulli(prob)
+                w = sgn * (y - pr);                                     // MCMCDerivRules.jl:111 chain, closed form
+            } else {
+                const double resid = y - e;                             // resid = Y - X*vars
+                const double z = resid * isn;
+                term = -0.5 * (z * z + kLog2Pi) - logsn;                // resid ~ Normal(0, sn)
+                w = resid * is2n;
+            }
+            const bool in = obs < M.n;
+            lik_part = in ? lik_part + term : lik_part;
+            rv[r] = in ? w : 0.0;
+            __builtin_amdgcn_sched_group_barrier(0x100, NM, 0);          // next chunk's operand reads first
+#pragma unroll
+            for (int sl = 0; sl < NM; ++sl) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // one MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, kVPM, 0);    // then VALU of the row
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (r < 3) {
+#pragma unroll
+                for (int sl = 0; sl < NM; ++sl) av[sl] = an[sl];
+            }
+        }
+        if (GRAD) {
+            // G tile T, k-slice kk: A[i][k] = X[obs 4kk+q][coord 16T+4(i&3)+(i>>2)], i = cl; kk outer so that
+            // consecutive MFMAs feed independent accumulators; operands one kk ahead
+            const double* gcol = L.X + b * XS + 4 * (p.cl & 3) + (p.cl >> 2);
+            double ga[NM];
+#pragma unroll
+            for (int T = 0; T < NM; ++T) ga[T] = gcol[p.q * S + 16 * T];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                double gn[NM];
+                if (kk < 3) {
+#pragma unroll
+                    for (int T = 0; T < NM; ++T) gn[T] = gcol[(4 * (kk + 1) + p.q) * S + 16 * T];
+                }
+#pragma unroll
+                for (int T = 0; T < NM; ++T) G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[T], rv[kk], G[T], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (kk < 3) {
+#pragma unroll
+                    for (int T = 0; T < NM; ++T) ga[T] = gn[T];
+                }
+            }
+        }
+        if (more) store_tile(b2);                             // held tile t-1: read before the last barrier
+        __syncthreads();
+        eta = eta_next;
+        b = b1;
+    }
+    return lik_part;
+}
+
+template <int NM, bool GRAD>
+__device__ __forceinline__ double glm_eval1(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
+                                         const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
+    const double lik_part = a.m.kind == MK_LOGISTIC ? glm_eval1_tiles<NM, GRAD, true>(a, p, L, x, G)
+                                                    : glm_eval1_tiles<NM, GRAD, false>(a, p, L, x, G);
+    return glm_finish<NM, 1, GRAD>(a, p, L, x, G, lik_part, oos);
+}
+
 // log-target and (GRAD) gradient of the regression model at the lane's coordinates x.
 // Every wave of the workgroup calls it the same number of times (barriers inside).
 // gout doubles as the MFMA accumulator of G = X^T r (G[T] covers slots 4T..4T+3).
 template <int NM, int NW, bool GRAD>
 __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
                                         const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
+    if constexpr (NW == 1) return glm_eval1<NM, GRAD>(a, p, L, x, G, oos);
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
     const int d = M.d;
@@ -272,32 +480,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         if (more) store_tile(b ^ 1);                          // the other buffer: its readers finished tile t-1
         __syncthreads();
     }
-    // likelihood: quarter combine, then slices left to right (each slice wave owns some rows)
-    const double lik = glm_sum(a, p, L, lik_part);
-    // prior vars ~ Normal(0, sp) over own coordinates
-    const double sp = M.prior_sigma, s2p = sp * sp, logsp = det_log(sp);
-    double pp = 0.0;
-#pragma unroll
-    for (int slot = 0; slot < (4 * NM); ++slot) {
-        const int k = own_coord(p, slot);
-        if (true && k < d) {
-            const double z = (x[slot] - 0.0) / sp;
-            pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
-        }
-    }
-    const double prior = glm_sum(a, p, L, pp);
-    double acc = 0.0 + prior;                                           // LLAcc(0.) + ...
-    bool bad = !(acc - acc == 0.0);
-    acc = acc + lik;
-    bad = bad || !(acc - acc == 0.0);
-    oos = bad;
-    if (bad) acc = -__builtin_inf();
-    if (GRAD) {
-#pragma unroll
-        for (int slot = 0; slot < (4 * NM); ++slot)
-            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - x[slot]) / s2p + G[slot >> 2][slot & 3];
-    }
-    return acc;
+    return glm_finish<NM, NW, GRAD>(a, p, L, x, G, lik_part, oos);
 }
 
 // ------------------------------------------------------------------ state access (layout [d][ld])
@@ -809,10 +992,10 @@ static unsigned glm_grid(int64_t C, const GlmShape& g) {
 }  // namespace mcmc
 
 mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
-    // d <= 64: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two);
-    // 64 < d <= 512: NW = 2, 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW.
+    // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1);
+    // 128 < d <= 512: NW = 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW.
     mcmc::GlmShape g{};
-    if (d <= 64) {
+    if (d <= 128) {
         int nm = 1;
         while (16 * nm < d) nm *= 2;
         g.nw = 1;
@@ -865,7 +1048,7 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& k, hipStream_t st) {
         case 11: return glm_step_nm<1, 1>(a, lds, grid, st);
         case 21: return glm_step_nm<2, 1>(a, lds, grid, st);
         case 41: return glm_step_nm<4, 1>(a, lds, grid, st);
-        case 42: return glm_step_nm<4, 2>(a, lds, grid, st);
+        case 81: return glm_step_nm<8, 1>(a, lds, grid, st);
         case 44: return glm_step_nm<4, 4>(a, lds, grid, st);
         case 48: return glm_step_nm<4, 8>(a, lds, grid, st);
         default: return hipErrorInvalidValue;
@@ -883,7 +1066,7 @@ hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& k, const double* xin, do
         case 11: glm_eval_kernel<1, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
         case 21: glm_eval_kernel<2, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
         case 41: glm_eval_kernel<4, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
-        case 42: glm_eval_kernel<4, 2><<<grid, glm_block<2>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 81: glm_eval_kernel<8, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
         case 44: glm_eval_kernel<4, 4><<<grid, glm_block<4>(), lds, st>>>(a, xin, lp, g, check); break;
         case 48: glm_eval_kernel<4, 8><<<grid, glm_block<8>(), lds, st>>>(a, xin, lp, g, check); break;
         default: return hipErrorInvalidValue;

@@ -148,11 +148,11 @@ static double orc_sum(const double* t, const orc_model* mdl, int order) {
 static orc_glm_geo orc_glm_geometry(const orc_model* m) {
     orc_glm_geo g;
     int nm = 1, nw = 1;
-    if (m->d <= 64) {
+    if (m->d <= 128) {                    /* one slice: glm.hip glm_eval1 */
         while (16 * nm < m->d) nm *= 2;
-    } else {
+    } else {                              /* d-slices of 64: glm_eval */
         nm = 4;
-        nw = 2;
+        nw = 4;
         while (64 * nw < m->d) nw *= 2;
     }
     g.ds = 16 * nm;
