@@ -47,7 +47,7 @@ CONFIGS = {
                         thinning=10, desc="config 3: logistic regression n=1000 d=128, MALA(0.001), "
                                           "262,144 chains"),
     "hmc1024": dict(model="iso", d=1024, chains=524288 // 8, sampler="hmc", steps=1000, warmup=100,
-                    thinning=100, desc="config 4: d=1024 iso-Normal, HMC(10, 0.1), 524,288 chains over 8 GPUs "
+                    thinning=20, desc="config 4: d=1024 iso-Normal, HMC(10, 0.1), 524,288 chains over 8 GPUs "
                                        "(65,536/GPU)"),
     "linear512": dict(model="linear", d=512, n=4096, chains=65536 // 8, sampler="hmcda", steps=20, warmup=2,
                       thinning=1, desc="config 5: linear regression n=4096 d=512, HMCDA(), 65,536 chains over 8 "
@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--strong", action="store_true", help="fixed total chains (--chains) split over ranks")
+    p.add_argument("--pcie", action="store_true", help="also time one run with host output buffers (kept samples "
+                                                       "cross PCIe after the loop); reported apart, never `value`")
     return p.parse_args()
 
 
@@ -147,28 +149,27 @@ def measured_traffic(wkey):
 
 
 def cpu_baseline(model, sampler, seconds, C=4096):
-    """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample."""
+    """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample; a one-chain
+    workload (config 1) is timed as one chain on one core."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref as orc
     import mcmchip as mc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    # calibrate on a short run (state set-up excluded), then size the timed sample to ~`seconds`
-    steps, dt = 2, 0.0
-    while dt < 0.5 and steps < 1 << 16:
-        steps *= 4
+    threads = max(1, min(threads, os.cpu_count() or 1, C))
+    # double the sample until one run takes about `seconds` / 2 (state set-up excluded); that last run is the
+    # sample -- same runner shape (burnin = steps/10, thinning 10) at every size, so an adaptive sampler's
+    # cost per step is measured as configured, and the wall time stays bounded (< ~2 x seconds in total)
+    steps, dt = 1, 0.0
+    while True:
         oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
         t0 = time.perf_counter()
-        oc.run(mc.SerialMC(steps=steps, burnin=1, thinning=1), nthreads=threads)
+        oc.run(mc.SerialMC(steps=steps, burnin=steps // 10, thinning=10 if steps >= 20 else 1), nthreads=threads)
         dt = time.perf_counter() - t0
-    rate = C * steps / dt
-    steps2 = max(steps, int(rate * seconds / C))
-    oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
-    t0 = time.perf_counter()
-    oc.run(mc.SerialMC(steps=steps2, burnin=max(1, steps2 // 10), thinning=10), nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": C * steps2 / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{C} chains x {steps2} steps of the same workload on the host ({dt:.1f} s), "
+        if dt >= seconds / 2 or steps >= 1 << 25:
+            break
+        steps *= 2 if dt > seconds / 16 else 4
+    return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{C} chains x {steps} steps of the same workload on the host ({dt:.1f} s), "
                       f"oracle/oracle.c OpenMP over chains; chains are independent, so the rate is per chain-step"}
 
 
@@ -223,6 +224,8 @@ def main():
     out.accept_bits = bits.data_ptr()
     out.on_device = 1
 
+    # library-owned output staging sized before the clock starts (the timed run allocates nothing)
+    _lib.check(lib.mcmc_chains_reserve_outputs(h, nkept, 0 if args.pcie else 1))
     if W > 0:
         wr = mc.SerialMC(steps=W, burnin=0, thinning=1)
         wout = _lib.Outputs()
@@ -253,12 +256,13 @@ def main():
     # ESS/sec: sum over chains of min over parameters of the IMSE ESS of the kept
     # samples, per second of sampling; computed on the device after the timed region, timed apart
     ess_line = None
-    if nkept >= 4:
+    if nkept >= 20:                     # the IMSE/IPSE estimators need a usable number of lags
         torch.cuda.synchronize(dev)
         te = time.perf_counter()
         ess = mc.stats.ess_device(samples, "imse")
-        # a chain that never moved has a 0/0 ESS (var.jl gives NaN); it counts as 0 effective samples
-        ess_min_sum = torch.nan_to_num(ess, nan=0.0).min(dim=0).values.sum()
+        # a chain that never moved has a 0/0 ESS (var.jl gives NaN), and an antithetic series whose first
+        # Geyer pair is <= 0 gets a negative IMSE variance (var.jl:53-57, m = 0): both count as 0 samples
+        ess_min_sum = torch.nan_to_num(ess, nan=0.0).clamp(min=0.0).min(dim=0).values.sum()
         torch.cuda.synchronize(dev)
         ess_s = time.perf_counter() - te
         if dist is not None:
@@ -266,9 +270,38 @@ def main():
             dist.all_reduce(ess_min_sum, op=dist.ReduceOp.SUM)
         ess_line = {"ess_per_sec": float(ess_min_sum) / T, "vtype": "imse", "kept_per_chain": nkept,
                     "sum_min_ess": float(ess_min_sum), "ess_compute_s": ess_s,
-                    "note": "sum_c min_j ESS_cj (ess.jl:6-10, Geyer IMSE) / sampling seconds; ESS on the GPU "
-                            "(kernels/stats.hip), outside the timed region"}
+                    "note": "sum_c min_j ESS_cj (ess.jl:6-10, Geyer IMSE; NaN or negative estimates count as 0) / "
+                            "sampling seconds; ESS on the GPU (kernels/stats.hip), outside the timed region"}
 
+    pcie = None
+    if args.pcie:
+        # the same run with caller-owned host buffers (C ABI on_device = 0): the kept samples, gradients and
+        # accept bits are copied to host memory after the step loop; pinned if the allocation succeeds
+        try:
+            hs = torch.empty((nkept, d, C), dtype=torch.float64, pin_memory=True)
+            hg = torch.empty((nkept, d, C), dtype=torch.float64, pin_memory=True) if grad_sampler else None
+            hb = torch.empty((nkept, (C + 63) // 64), dtype=torch.int64, pin_memory=True)
+            kind = "pinned"
+        except RuntimeError:
+            hs = torch.empty((nkept, d, C), dtype=torch.float64)
+            hg = torch.empty((nkept, d, C), dtype=torch.float64) if grad_sampler else None
+            hb = torch.empty((nkept, (C + 63) // 64), dtype=torch.int64)
+            kind = "pageable"
+        hout = _lib.Outputs()
+        hout.samples = hs.data_ptr()
+        hout.gradients = hg.data_ptr() if hg is not None else None
+        hout.accept_bits = hb.data_ptr()
+        hout.on_device = 0
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(hout)))
+        Tp = time.perf_counter() - t0
+        pcie = {"value": C * world * K / Tp, "unit": "chain-steps/s", "ms_per_step": Tp * 1e3 / K,
+                "host_buffers": kind, "bytes_to_host": int(hs.numel() * 8 + (hg.numel() * 8 if hg is not None else 0)
+                                                          + hb.numel() * 8),
+                "note": "the same workload with host output buffers: the step loop plus the device-to-host copy "
+                        "of the kept outputs after it"}
+        del hs, hg, hb
     spl = args.spl if args.spl >= 0 else 0
     launches = 1 if spl == 0 else -(-K // spl)
     # per-GPU workload key: the PMC traffic of a committed rocprofv3 run of this same workload
@@ -329,9 +362,11 @@ def main():
         "roofline": roof,
         "ess": ess_line,
     }
+    if pcie is not None:
+        line["pcie_inclusive"] = pcie
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,
-                                            C=4096 if cfg0["model"] == "iso" else 256)
+                                            C=min(C, 4096 if cfg0["model"] == "iso" else 64))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -191,6 +191,10 @@ int mcmc_chains_ram_factor(mcmc_chains* chains, double* S);
 int mcmc_chains_set_steps_per_launch(mcmc_chains* chains, int64_t steps_per_launch);
 /* store gradients of kept samples for gradient samplers (default 1, SerialMC.jl:51-53) */
 int mcmc_chains_set_store_gradients(mcmc_chains* chains, int32_t store);
+/* pre-size the library's own output buffers for runs keeping up to nkept steps (staging of the
+ * wave-per-chain layout; device copies when on_device == 0), so that mcmc_run_serialmc allocates
+ * nothing (no reference counterpart: the Julia runner grows its DataFrame per run, SerialMC.jl:39-42). */
+int mcmc_chains_reserve_outputs(mcmc_chains* chains, int64_t nkept, int32_t on_device);
 
 /* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
 int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);

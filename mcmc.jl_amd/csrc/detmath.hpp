@@ -64,47 +64,73 @@ __device__ __forceinline__ double uniform32(uint32_t a) { return (double)a * 0x1
 __device__ __forceinline__ double pow2i(int k) { return bits2d((uint64_t)(k + 1023) << 52); }
 
 // fdlibm e_log.c general path.  Special cases resolved by selects so the
-// common path stays branch-free across the wave.
-__device__ __forceinline__ double det_log(double x) {
-    const double ln2_hi = 0x1.62e42fee00000p-1;
-    const double ln2_lo = 0x1.a39ef35793c76p-33;
-    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2,
-                 Lg3 = 0x1.2492494229359p-2, Lg4 = 0x1.c71c51d8e78afp-3,
-                 Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
-                 Lg7 = 0x1.2f112df3e5244p-3;
+// common path stays branch-free across the wave.  Written as stages (det_log = s1, s2, s3, fin) so that a
+// caller can interleave independent work between them (glm.hip); the operations are the same either way.
+struct LogState {
+    double x, m, f, s, dk, z, w, R;
+    uint64_t bx;
+    int k;
+};
+__device__ __forceinline__ void det_log_s1(double x, LogState& L) {   // reduction to m in [sqrt(2)/2, sqrt(2))
     uint64_t bx = d2bits(x);
-    int k = 0;
     const bool sub = bx < 0x0010000000000000ull;            // zero or subnormal (or negative: handled below)
     const bool scl = sub && x > 0.0;                         // subnormal: scale by 2^54 (selects, no branch)
     x = scl ? x * 0x1p54 : x;
-    k = scl ? -54 : 0;
+    int k = scl ? -54 : 0;
     bx = d2bits(x);
     uint32_t hx = (uint32_t)(bx >> 32);
     k += (int)((hx >> 20) & 0x7ff) - 1023;
     hx &= 0x000fffffu;
     const uint32_t i = (hx + 0x95f64u) & 0x100000u;
     const uint64_t nb = ((uint64_t)(hx | (i ^ 0x3ff00000u)) << 32) | (bx & 0xffffffffull);
-    const double m = bits2d(nb);
-    k += (int)(i >> 20);
-    const double f = m - 1.0;
-    const double s = f / (2.0 + f);
-    const double dk = (double)k;
-    const double z = s * s;
-    const double w = z * z;
-    const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
-    const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
-    const double R = t2 + t1;
-    const double hfsq = 0.5 * f * f;
-    double res = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    L.m = bits2d(nb);
+    L.k = k + (int)(i >> 20);
+    L.x = x;
+    L.bx = bx;
+}
+__device__ __forceinline__ void det_log_s2(LogState& L) {             // s = f / (2 + f)
+    L.f = L.m - 1.0;
+    L.s = L.f / (2.0 + L.f);
+    L.dk = (double)L.k;
+}
+__device__ __forceinline__ void det_log_s3(LogState& L) {             // R(z), z = s^2
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2,
+                 Lg3 = 0x1.2492494229359p-2, Lg4 = 0x1.c71c51d8e78afp-3,
+                 Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    L.z = L.s * L.s;
+    L.w = L.z * L.z;
+    const double t1 = L.w * __builtin_fma(L.w, __builtin_fma(L.w, Lg6, Lg4), Lg2);
+    const double t2 = L.z * __builtin_fma(L.w, __builtin_fma(L.w, __builtin_fma(L.w, Lg7, Lg5), Lg3), Lg1);
+    L.R = t2 + t1;
+}
+__device__ __forceinline__ double det_log_fin(const LogState& L) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double x = L.x;
+    const double hfsq = 0.5 * L.f * L.f;
+    double res = L.dk * ln2_hi - ((hfsq - (L.s * (hfsq + L.R) + L.dk * ln2_lo)) - L.f);
     // special values, in the oracle's order: NaN, negative, zero, +inf
     if (x == 0.0) res = -__builtin_inf();
-    if (bx >= 0x7ff0000000000000ull && x > 0.0) res = x;     // +inf
+    if (L.bx >= 0x7ff0000000000000ull && x > 0.0) res = x;     // +inf
     if (x < 0.0) res = bits2d(0x7ff8000000000000ull);
     if (x != x) res = x;
     return res;
 }
+__device__ __forceinline__ double det_log(double x) {
+    LogState L;
+    det_log_s1(x, L);
+    det_log_s2(L);
+    det_log_s3(L);
+    return det_log_fin(L);
+}
 
-__device__ __forceinline__ double det_exp(double x) {
+// Cody-Waite reduction + degree-13 Taylor polynomial; stages as det_log.
+struct ExpState {
+    double x, xc, r, p;
+    int k;
+};
+__device__ __forceinline__ void det_exp_s1(double x, ExpState& E) {   // k = round(x / ln2), r = x - k ln2
     const double inv_ln2 = 0x1.71547652b82fep+0;
     const double ln2_hi = 0x1.62e42fee00000p-1;
     const double ln2_lo = 0x1.a39ef35793c76p-33;
@@ -112,10 +138,15 @@ __device__ __forceinline__ double det_exp(double x) {
     const double xc = __builtin_fmin(__builtin_fmax(x, -746.0), 710.0);  // keep k in range for NaN-free math
     const double t = __builtin_fma(xc, inv_ln2, shifter);
     const double kd = t - shifter;
-    const int k = (int)kd;
+    E.k = (int)kd;
     double r = __builtin_fma(-kd, ln2_hi, xc);
-    r = __builtin_fma(-kd, ln2_lo, r);
-    double p = 0x1.6124613a86d09p-33;
+    E.r = __builtin_fma(-kd, ln2_lo, r);
+    E.x = x;
+    E.p = 0x1.6124613a86d09p-33;
+}
+__device__ __forceinline__ void det_exp_s2(ExpState& E) {             // Horner, first half
+    double p = E.p;
+    const double r = E.r;
     p = __builtin_fma(p, r, 0x1.1eed8eff8d898p-29);
     p = __builtin_fma(p, r, 0x1.ae64567f544e4p-26);
     p = __builtin_fma(p, r, 0x1.27e4fb7789f5cp-22);
@@ -123,18 +154,34 @@ __device__ __forceinline__ double det_exp(double x) {
     p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-16);
     p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-13);
     p = __builtin_fma(p, r, 0x1.6c16c16c16c17p-10);
+    E.p = p;
+}
+__device__ __forceinline__ void det_exp_s3(ExpState& E) {             // Horner, second half
+    double p = E.p;
+    const double r = E.r;
     p = __builtin_fma(p, r, 0x1.1111111111111p-7);
     p = __builtin_fma(p, r, 0x1.5555555555555p-5);
     p = __builtin_fma(p, r, 0x1.5555555555555p-3);
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     p = __builtin_fma(p, r, 1.0);
-    const int k1 = k / 2, k2 = k - k1;
-    double res = (p * pow2i(k1)) * pow2i(k2);
+    E.p = p;
+}
+__device__ __forceinline__ double det_exp_fin(const ExpState& E) {
+    const int k1 = E.k / 2, k2 = E.k - k1;
+    double res = (E.p * pow2i(k1)) * pow2i(k2);
+    const double x = E.x;
     if (x > 709.782712893384) res = __builtin_inf();
     if (x < -745.1332191019412) res = 0.0;
     if (x != x) res = x;
     return res;
+}
+__device__ __forceinline__ double det_exp(double x) {
+    ExpState E;
+    det_exp_s1(x, E);
+    det_exp_s2(E);
+    det_exp_s3(E);
+    return det_exp_fin(E);
 }
 
 __device__ __forceinline__ void det_sincos2pi(double u, double& s_out, double& c_out) {

@@ -734,6 +734,29 @@ extern "C" int mcmc_chains_set_store_gradients(mcmc_chains* c, int32_t store) {
     return MCMC_OK;
 }
 
+// Pre-size the library-owned output buffers of a run keeping nkept steps (the wave-per-chain staging
+// rows, and the device copies used when the caller's buffers are on the host), so that the run itself
+// allocates nothing.  Buffers only grow; they are freed with the chains.
+extern "C" int mcmc_chains_reserve_outputs(mcmc_chains* c, int64_t nkept, int32_t on_device) {
+    if (!c || nkept < 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    if (int rc = set_device(c->model->ctx)) return rc;
+    const size_t d = (size_t)c->model->args.d, C = (size_t)c->C, nk = (size_t)nkept;
+    const bool grads = c->sa.kind != SK_RWM && c->sa.kind != SK_RAM && c->store_grads;
+    if (c->layout == LAYOUT_WPC) {
+        const size_t nstage = nk * C * (size_t)c->ld;
+        if (int rc = ensure(c->stage_samples, nstage * 8)) return rc;
+        if (grads)
+            if (int rc = ensure(c->stage_grads, nstage * 8)) return rc;
+    }
+    if (!on_device) {
+        if (int rc = ensure(c->out_samples, nk * d * C * 8)) return rc;
+        if (grads)
+            if (int rc = ensure(c->out_grads, nk * d * C * 8)) return rc;
+        if (int rc = ensure(c->out_bits, nk * ((C + 63) / 64) * 8)) return rc;
+    }
+    return MCMC_OK;
+}
+
 // ------------------------------------------------------------------ run
 extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs* out) {
     if (!c || !r) return fail(MCMC_E_INVALID_ARG, "NULL argument");

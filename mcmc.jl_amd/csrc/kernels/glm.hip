@@ -247,60 +247,61 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         const bool more = t + 2 < ntiles;
         if (more) load_tile(t + 2);
         const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;
-        // eta_{t+1} (buffer b1; garbage past the last tile, unused) in four chunks of NM k-slices, each
-        // beside one observation row's elementwise work on eta_t: the chunk's MFMAs and the row's VALU
-        // chain are independent and interleave (scheduling groups: one MFMA, then up to kVPM VALU).  A
-        // chunk's LDS operands are read one chunk ahead, so no MFMA waits on its ds_read.
-        constexpr int kVPM = LOGI ? (NM >= 8 ? 12 : 24) : 4;
+        // eta_{t+1} (buffer b1; garbage past the last tile, unused) interleaved with the elementwise work on
+        // eta_t by hand: the four rows' work runs in stages (det_exp / det_log split at their natural points,
+        // the same operations), 32 sub-stages (stage, row) per tile, and sub-stage j is preceded by the
+        // eta MFMAs [j KM / 32, (j+1) KM / 32), KM = 4 NM; a scheduling fence after every sub-stage keeps that
+        // order (an in-order wave can only overlap a dependent MFMA chain with VALU placed between its MFMAs).
+        // The eta operands are read from LDS kLA MFMAs ahead.
+        constexpr int KM = 4 * NM;
+        constexpr int kLA = 4;
         f64x4 eta_next = f64x4{0.0, 0.0, 0.0, 0.0};
         const double* xrow1 = L.X + b1 * XS + p.cl * S + 4 * p.q;
         const double* LY = L.Y + b * 16;
-        double rv[4];
-        double av[NM];
+        double av[KM];
 #pragma unroll
-        for (int sl = 0; sl < NM; ++sl) av[sl] = xrow1[16 * (sl >> 2) + (sl & 3)];
+        for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow1[16 * (m >> 2) + (m & 3)];
+        double y[4], ea[4], pr[4], term[4], rv[4];
+        ExpState E[4];
+        LogState Lg[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double an[NM];
-            if (r < 3) {
+        for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
+        constexpr int NSTAGE = LOGI ? 8 : 1;
 #pragma unroll
-                for (int sl = 0; sl < NM; ++sl) {
-                    const int slot = (r + 1) * NM + sl;
-                    an[sl] = xrow1[16 * (slot >> 2) + (slot & 3)];
-                }
+        for (int j = 0; j < 4 * NSTAGE; ++j) {
+            const int st = j >> 2, r = j & 3;
+#pragma unroll
+            for (int m = j * KM / (4 * NSTAGE); m < (j + 1) * KM / (4 * NSTAGE); ++m) {
+                if (m + kLA < KM) av[m + kLA] = xrow1[16 * ((m + kLA) >> 2) + ((m + kLA) & 3)];
+                eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x[m], eta_next, 0, 0, 0);
             }
-            const double y = LY[p.q + 4 * r];
-#pragma unroll
-            for (int sl = 0; sl < NM; ++sl)
-                eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[sl], x[r * NM + sl], eta_next, 0, 0, 0);
-            const double e = eta[r];
-            const int64_t obs = t * 16 + p.q + 4 * r;
-            double term, w;
             if (LOGI) {
-                const double tt = det_exp(-(sgn * e));                  // prob = 1/(1+exp(-X*vars))
-                const double pr = 1.0 / (1.0 + tt);
-                term = det_log((y >= 0.5) ? pr : 1.0 - pr);             // Y ~ Bernoulli(prob)
-                w = sgn * (y - pr);                                     // MCMCDerivRules.jl:111 chain, closed form
+                switch (st) {
+                    case 0: det_exp_s1(-(sgn * eta[r]), E[r]); break;               // prob = 1/(1+exp(-X*vars))
+                    case 1: det_exp_s2(E[r]); break;
+                    case 2: det_exp_s3(E[r]); break;
+                    case 3: ea[r] = det_exp_fin(E[r]); pr[r] = 1.0 / (1.0 + ea[r]); break;
+                    case 4: det_log_s1((y[r] >= 0.5) ? pr[r] : 1.0 - pr[r], Lg[r]); break;   // Y ~ Bernoulli(prob)
+                    case 5: det_log_s2(Lg[r]); break;
+                    case 6: det_log_s3(Lg[r]); break;
+                    default:
+                        term[r] = det_log_fin(Lg[r]);
+                        rv[r] = sgn * (y[r] - pr[r]);                           // MCMCDerivRules.jl:111, closed form
+                        break;
+                }
             } else {
-                const double resid = y - e;                             // resid = Y - X*vars
+                const double resid = y[r] - eta[r];                             // resid = Y - X*vars
                 const double z = resid * isn;
-                term = -0.5 * (z * z + kLog2Pi) - logsn;                // resid ~ Normal(0, sn)
-                w = resid * is2n;
-            }
-            const bool in = obs < M.n;
-            lik_part = in ? lik_part + term : lik_part;
-            rv[r] = in ? w : 0.0;
-            __builtin_amdgcn_sched_group_barrier(0x100, NM, 0);          // next chunk's operand reads first
-#pragma unroll
-            for (int sl = 0; sl < NM; ++sl) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // one MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, kVPM, 0);    // then VALU of the row
+                term[r] = -0.5 * (z * z + kLog2Pi) - logsn;                     // resid ~ Normal(0, sn)
+                rv[r] = resid * is2n;
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (r < 3) {
+        }
 #pragma unroll
-                for (int sl = 0; sl < NM; ++sl) av[sl] = an[sl];
-            }
+        for (int r = 0; r < 4; ++r) {                                           // the lane's terms in (t, r) order
+            const bool in = t * 16 + p.q + 4 * r < M.n;
+            lik_part = in ? lik_part + term[r] : lik_part;
+            rv[r] = in ? rv[r] : 0.0;
         }
         if (GRAD) {
             // G tile T, k-slice kk: A[i][k] = X[obs 4kk+q][coord 16T+4(i&3)+(i>>2)], i = cl; kk outer so that

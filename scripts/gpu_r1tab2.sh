@@ -1,0 +1,20 @@
+# Round-1 results table, second part (bounded CPU baselines for the regression configs).
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+make -C oracle -s
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "$name exit $rc" | tee -a "$O/steps.txt"
+  case $rc in 0|1|2|5) return 0;; *) echo "fatal rc $rc in $name: stopping"; exit $rc;; esac
+}
+step tab_readme 150 python3 bench.py --config readme
+step tab_log128 150 python3 bench.py --config logistic128
+step tab_h1024 150 python3 bench.py --config hmc1024
+step tab_lin512 150 python3 bench.py --config linear512
+step tab_mala32 150 python3 bench.py --no-cpu-baseline --sampler mala
+step tab_hmc32 150 python3 bench.py --no-cpu-baseline --sampler hmc
+echo all-done
