@@ -25,7 +25,7 @@ end
 
 const MODEL_ISO_NORMAL_DOT, MODEL_NORMAL_DSL, MODEL_LOGISTIC, MODEL_LINEAR = 1, 2, 3, 4
 const MODEL_ABS_NORMAL_DSL, MODEL_DIST_DSL = 5, 6
-const RWM_K, MALA_K, HMC_K, HMCDA_K = 1, 2, 3, 4
+const RWM_K, MALA_K, HMC_K, HMCDA_K, RAM_K = 1, 2, 3, 4, 5
 
 check(st) = st == 0 ? nothing :
     error(unsafe_string(ccall((:mcmc_last_error, lib), Cstring, ())))   # reference @assert text
@@ -61,6 +61,7 @@ rwm(scale) = SamplerCfg(RWM_K, scale, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 hmc(n, eps) = SamplerCfg(HMC_K, 0, 0, n, eps, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 hmcda(; rate=0.65, len=2., shrinkage=0.05, t0=10., step=0.75) =
     SamplerCfg(HMCDA_K, 0, 0, 0, 0, rate, len, shrinkage, t0, step, 0, 0, 0, 0, 0, 0)
+ram(scale = 1.0, rate = 0.234) = SamplerCfg(RAM_K, scale, 0, 0, 0, rate, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)   # RAM.jl:22-34
 
 function chains(model, s::SamplerCfg, nchains; seed = 1, offset = 0)
     h = Ref{Ptr{Cvoid}}(C_NULL)
@@ -69,6 +70,10 @@ function chains(model, s::SamplerCfg, nchains; seed = 1, offset = 0)
         model, s, nchains, offset, seed, C_NULL, h))
     h[]
 end
+
+# optional: size the library's staging buffers once, so that timed runs allocate nothing
+reserve(ch, nkept; on_device = false) =
+    check(ccall((:mcmc_chains_reserve_outputs, lib), Cint, (Ptr{Cvoid}, Int64, Int32), ch, nkept, on_device))
 
 # run_serialmc (SerialMC.jl:37-85): returns samples[nkept][d][C] (Julia: Array{Float64,3} of size (C, d, nkept))
 function run_serialmc(ch, d, C; steps, burnin = 0, thinning = 1)
