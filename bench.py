@@ -125,6 +125,8 @@ def hbm_bytes_per_unit(d, sampler):
 
 def kernel_name(cfg, d, sampler):
     if cfg["model"] != "iso":
+        if sampler == "mala" and d <= 128:
+            return f"glm_mala1<{next(m for m in (1, 2, 4, 8) if 16 * m >= d)}>"
         nm = 1
         while d <= 128 and 16 * nm < d:
             nm *= 2
@@ -303,7 +305,9 @@ def main():
                         "of the kept outputs after it"}
         del hs, hg, hb
     spl = args.spl if args.spl >= 0 else 0
-    launches = 1 if spl == 0 else -(-K // spl)
+    nl = ct.c_int64(0)
+    _lib.check(lib.mcmc_chains_launches(h, K, ct.byref(nl)))
+    launches = nl.value                                  # the library's plan (some kernels fuse one step)
     # per-GPU workload key: the PMC traffic of a committed rocprofv3 run of this same workload
     # (profiles/traffic.json, written by scripts/summarize_prof.py) fills roofline.traffic
     wkey = f"{args.config}|d={d}|chains={C}|{args.sampler}|steps={K}|thinning={args.thinning}|spl={spl}"

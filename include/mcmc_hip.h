@@ -195,6 +195,9 @@ int mcmc_chains_set_store_gradients(mcmc_chains* chains, int32_t store);
  * wave-per-chain layout; device copies when on_device == 0), so that mcmc_run_serialmc allocates
  * nothing (no reference counterpart: the Julia runner grows its DataFrame per run, SerialMC.jl:39-42). */
 int mcmc_chains_reserve_outputs(mcmc_chains* chains, int64_t nkept, int32_t on_device);
+/* kernel launches a run of len steps takes (steps per launch as set, capped by kernels that fuse a
+ * bounded number of steps); for timing per launch. */
+int mcmc_chains_launches(mcmc_chains* chains, int64_t len, int64_t* launches);
 
 /* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
 int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);

@@ -43,6 +43,8 @@ hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t 
                            int64_t batchlen, double* ess, double* var, hipStream_t st);
 // padded covariate row length the regression kernels read (X_pad is [n_pad][d_pad])
 int mcmc_glm_d_pad(int d);
+// steps one launch of the regression step kernel may fuse (0: any)
+int mcmc_glm_steps_per_launch(int d, int64_t n, int sampler_kind);
 
 hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st);
 hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st);

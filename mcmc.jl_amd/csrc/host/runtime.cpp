@@ -734,6 +734,24 @@ extern "C" int mcmc_chains_set_store_gradients(mcmc_chains* c, int32_t store) {
     return MCMC_OK;
 }
 
+// steps fused per launch for a run of len steps: the user's setting (0: the whole run), capped by the
+// kernels that fuse a bounded number of steps (the single-slice regression MALA kernel: one)
+static int64_t launch_steps(const mcmc_chains* c, int64_t len) {
+    int64_t spl = c->spl > 0 ? c->spl : len;
+    if (c->layout == LAYOUT_GLM) {
+        const int64_t kmax = mcmc_glm_steps_per_launch(c->model->args.d, c->model->args.n, c->sa.kind);
+        if (kmax > 0 && spl > kmax) spl = kmax;
+    }
+    return spl < 1 ? 1 : spl;
+}
+
+extern "C" int mcmc_chains_launches(mcmc_chains* c, int64_t len, int64_t* launches) {
+    if (!c || !launches || len < 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    const int64_t spl = launch_steps(c, len);
+    *launches = len == 0 ? 0 : (len + spl - 1) / spl;
+    return MCMC_OK;
+}
+
 // Pre-size the library-owned output buffers of a run keeping nkept steps (the wave-per-chain staging
 // rows, and the device copies used when the caller's buffers are on the host), so that the run itself
 // allocates nothing.  Buffers only grow; they are freed with the chains.
@@ -840,7 +858,7 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     s.nw = nw;
     s.n_evals = c->d_evals;
 
-    const int64_t spl = c->spl > 0 ? c->spl : r->len;
+    const int64_t spl = launch_steps(c, r->len);
     HIP_TRY(hipStreamSynchronize(st));
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventRecord(ctx->ev0, st));

@@ -94,6 +94,7 @@ struct GlmLds {
     double* scal;
     double* rbuf;     // [4 tiles][4 r][64 lanes]: residual weights of a tile, exchanged between slice waves
     int* iscr;
+    double* beta;     // single-slice kernels: [4 waves][4 NM slots][64 lanes], a lane's proposal coordinates
 };
 
 __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
@@ -104,11 +105,13 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     L.scal = L.part + kGlmMaxWaves * 64 * 4;
     L.rbuf = L.scal + kGlmMaxWaves * 16;
     L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
+    L.beta = L.rbuf + 4 * 4 * 64 + 2;                // after the 4 ints of iscr
     return L;
 }
 
 size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(glm_xbufs(g.nw) * 16 * g.lds_stride + glm_xbufs(g.nw) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 + 4 * 4 * 64 + 4) * 8;
+    return (size_t)(glm_xbufs(g.nw) * 16 * g.lds_stride + glm_xbufs(g.nw) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
+                    4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8;
 }
 
 // sum of a per-chain quantity held as 4 quarter partials per wave and NW slice partials:
@@ -138,11 +141,23 @@ __device__ __forceinline__ int64_t glm_max(const GlmLds& L, int64_t v, bool live
     return r;
 }
 
+// The lane's coordinates of the evaluation point: held in registers (XArr) or in the lane's private
+// LDS slots (XLds: slot s at b[64 s], b = L.beta + (wave * 4 NM) * 64 + lane).
+template <int NS>
+struct XArr {
+    const double (&v)[NS];
+    __device__ __forceinline__ double operator()(int s) const { return v[s]; }
+};
+struct XLds {
+    const double* b;
+    __device__ __forceinline__ double operator()(int s) const { return b[64 * s]; }
+};
+
 // The end of an evaluation: likelihood partials combined (quarters, then slices left to right), the
 // prior vars ~ Normal(0, sp) over own coordinates, the LLAcc rule, and the prior's gradient added to G.
-template <int NM, int NW, bool GRAD>
+template <int NM, int NW, bool GRAD, class XA>
 __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
-                                          const double (&x)[(4 * NM)], f64x4 (&G)[NM], double lik_part, bool& oos) {
+                                          const XA& x, f64x4 (&G)[NM], double lik_part, bool& oos) {
     const ModelArgs& M = a.m;
     const int d = M.d;
     const double lik = glm_sum(a, p, L, lik_part);
@@ -153,7 +168,7 @@ __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, 
     for (int slot = 0; slot < (4 * NM); ++slot) {
         const int k = own_coord(p, slot);
         if (true && k < d) {
-            const double z = (x[slot] - 0.0) / sp;
+            const double z = (x(slot) - 0.0) / sp;
             pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
         }
     }
@@ -167,7 +182,7 @@ __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, 
     if (GRAD) {
 #pragma unroll
         for (int slot = 0; slot < (4 * NM); ++slot)
-            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - x[slot]) / s2p + G[slot >> 2][slot & 3];
+            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - x(slot)) / s2p + G[slot >> 2][slot & 3];
     }
     return acc;
 }
@@ -181,9 +196,9 @@ __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, 
 //                   one barrier
 // The arithmetic is glm_eval's, operation for operation (eta chains over (m, e, q); G chains over
 // observations; a lane's likelihood terms in (t, r) order), so the oracle's orc_glm_eval restates both.
-template <int NM, bool GRAD, bool LOGI>
+template <int NM, bool GRAD, bool LOGI, class XA>
 __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
-                                                const double (&x)[(4 * NM)], f64x4 (&G)[NM]) {
+                                                const XA& x, f64x4 (&G)[NM]) {
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
     const int S = g.lds_stride;
@@ -227,7 +242,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         const double* xrow = L.X + b * XS + p.cl * S + 4 * p.q;
 #pragma unroll
         for (int slot = 0; slot < (4 * NM); ++slot)
-            e = __builtin_amdgcn_mfma_f64_16x16x4f64(xrow[16 * (slot >> 2) + (slot & 3)], x[slot], e, 0, 0, 0);
+            e = __builtin_amdgcn_mfma_f64_16x16x4f64(xrow[16 * (slot >> 2) + (slot & 3)], x(slot), e, 0, 0, 0);
         return e;
     };
     load_tile(0);
@@ -273,7 +288,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
 #pragma unroll
             for (int m = j * KM / (4 * NSTAGE); m < (j + 1) * KM / (4 * NSTAGE); ++m) {
                 if (m + kLA < KM) av[m + kLA] = xrow1[16 * ((m + kLA) >> 2) + ((m + kLA) & 3)];
-                eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x[m], eta_next, 0, 0, 0);
+                eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x(m), eta_next, 0, 0, 0);
             }
             if (LOGI) {
                 switch (st) {
@@ -334,9 +349,9 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
     return lik_part;
 }
 
-template <int NM, bool GRAD>
+template <int NM, bool GRAD, class XA>
 __device__ __forceinline__ double glm_eval1(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
-                                         const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
+                                         const XA& x, f64x4 (&G)[NM], bool& oos) {
     const double lik_part = a.m.kind == MK_LOGISTIC ? glm_eval1_tiles<NM, GRAD, true>(a, p, L, x, G)
                                                     : glm_eval1_tiles<NM, GRAD, false>(a, p, L, x, G);
     return glm_finish<NM, 1, GRAD>(a, p, L, x, G, lik_part, oos);
@@ -348,7 +363,7 @@ __device__ __forceinline__ double glm_eval1(const GlmArgs& a, const GlmPos& p, c
 template <int NM, int NW, bool GRAD>
 __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
                                         const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
-    if constexpr (NW == 1) return glm_eval1<NM, GRAD>(a, p, L, x, G, oos);
+    if constexpr (NW == 1) return glm_eval1<NM, GRAD>(a, p, L, XArr<4 * NM>{x}, G, oos);
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
     const int d = M.d;
@@ -481,7 +496,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         if (more) store_tile(b ^ 1);                          // the other buffer: its readers finished tile t-1
         __syncthreads();
     }
-    return glm_finish<NM, NW, GRAD>(a, p, L, x, G, lik_part, oos);
+    return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, lik_part, oos);
 }
 
 // ------------------------------------------------------------------ state access (layout [d][ld])
@@ -848,6 +863,126 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_mala(GlmArgs a) {
     glm_count_evals(a, p, s.nsteps);
 }
 
+// MALA on one slice (d <= 128): as glm_mala, with the proposal kept in the lane's private LDS slots
+// (L.beta) instead of registers -- built block by block from the normals and the state in HBM, read by
+// the eta MFMAs as their B operands and by the backward density afterwards -- so that only the
+// gradient accumulators live across the tile loop.  One launch is one step: inside a step loop the
+// compiler hoists the tile loop's invariant addresses and constants out of it and the kernel spills
+// (> 512 registers); the per-chain scalars (lp, tuner state) round-trip through HBM per launch instead.
+// Same operations in the same order as glm_mala.
+template <int NM>
+__global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int NS = 4 * NM;
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const GlmPos p = glm_pos(a);
+    const GlmLds L = glm_lds(a, smem);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int64_t cc = p.live ? p.c : 0;
+    double* const xb = L.beta + (size_t)(p.wave * NS) * 64 + p.lane;
+    const size_t ld = (size_t)s.ld;
+    const double* const xl = glm_lane_ptr(p, a.st.x, s.ld, cc);
+    const double* const gl = glm_lane_ptr(p, a.st.g, s.ld, cc);
+    double lp = a.st.lp[cc];
+    double h = sa.tuner ? a.st.t_step[cc] : sa.drift_step;
+    int32_t n_acc = sa.tuner ? a.st.t_acc[cc] : 0;
+    int32_t n_prop = sa.tuner ? a.st.t_prop[cc] : 0;
+    {                                   // ONE step per launch (mcmc_glm_steps_per_launch): no step loop
+        const int t = 0;
+        const int64_t i = s.step_begin + t;
+        if (sa.tuner) n_prop += 1;
+        const double half = h / 2.0;
+        const double sq = __builtin_sqrt(h);
+        const double twoh = 2.0 * h;
+        const double Lc = det_log(kTwoPi * h) / 2.0;
+        double qf = 0.0;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const uint32_t blk = (uint32_t)((p.base >> 2) + 4 * m + p.q);      // coords 4*blk .. 4*blk+3
+            const u32x4 w = rs.block(chain, (uint32_t)i, blk, TAG_NORMAL);
+            double z[4];
+            normals4(w, z[0], z[1], z[2], z[3]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int slot = 4 * m + e;
+                const bool v = glm_valid(a, p, slot);
+                const size_t o = (size_t)(16 * m + e) * ld;
+                const double xv = v ? xl[o] : 0.0;
+                const double gv = v ? gl[o] : 0.0;
+                const double pm = xv + half * gv;                               // MALA.jl:98
+                const double xpv = pm + sq * (v ? z[e] : 0.0);                  // MALA.jl:100
+                const double ee = pm - xpv;
+                if (v) qf = qf + ((-(ee * ee)) / twoh - Lc);                    // MALA.jl:103
+                xb[64 * slot] = xpv;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        qf = glm_sum(a, p, L, qf);
+        bool oos;
+        f64x4 gp[NM];
+        const double lpp = glm_eval1<NM, true>(a, p, L, XLds{xb}, gp, oos);    // MALA.jl:101
+        double qb = 0.0;
+#pragma unroll
+        for (int slot = 0; slot < NS; ++slot) {
+            const bool v = glm_valid(a, p, slot);
+            const double xv = v ? xl[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
+            const double e = (xb[64 * slot] + half * gp[slot >> 2][slot & 3]) - xv;   // MALA.jl:104-105
+            if (v) qb = qb + ((-(e * e)) / twoh - Lc);
+        }
+        qb = glm_sum(a, p, L, qb);
+        const double ratio = ((lpp + qb) - lp) - qf;                   // MALA.jl:107
+        const bool acc = glm_mh_short_circuit(rs, chain, (uint32_t)i, ratio);
+        int64_t kk;
+        const bool kept = kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk);
+        double* const ks = kept && s.samples ? s.samples + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
+        double* const kg = kept && s.grads ? s.grads + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
+        if (p.live) {
+            double* const xw = a.st.x + (size_t)(p.base + 4 * p.q) * ld + (size_t)p.c;
+            double* const gw = a.st.g + (size_t)(p.base + 4 * p.q) * ld + (size_t)p.c;
+            const size_t Cs = (size_t)s.C;
+#pragma unroll
+            for (int slot = 0; slot < NS; ++slot) {
+                if (!glm_valid(a, p, slot)) continue;
+                const size_t r = (size_t)(16 * (slot >> 2) + (slot & 3));
+                double xv, gv;
+                if (acc) {
+                    xv = xb[64 * slot];
+                    gv = gp[slot >> 2][slot & 3];
+                    xw[r * ld] = xv;
+                    gw[r * ld] = gv;
+                } else {
+                    xv = xl[r * ld];
+                    gv = gl[r * ld];
+                }
+                const size_t ko = (size_t)(p.base + 4 * p.q + r) * Cs + (size_t)p.c;
+                if (ks) ks[ko] = xv;
+                if (kg) kg[ko] = gv;
+            }
+        }
+        if (acc) {
+            lp = lpp;
+            if (sa.tuner) n_acc += 1;
+        }
+        if (kept) glm_store_bit(a, p, kk, acc);
+        if (sa.tuner && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // MALA.jl:116-118
+            h = h * glm_tune_factor(n_acc, n_prop, sa.target_rate);
+            n_acc = 0;
+            n_prop = 0;
+        }
+    }
+    if (p.live && p.q == 0 && p.slice == 0) {
+        a.st.lp[p.c] = lp;
+        if (sa.tuner) {
+            a.st.t_step[p.c] = h;
+            a.st.t_acc[p.c] = n_acc;
+            a.st.t_prop[p.c] = n_prop;
+        }
+    }
+    glm_count_evals(a, p, s.nsteps);
+}
+
 template <int NM, int NW, bool DA>
 __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1017,6 +1152,13 @@ mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
 
 int mcmc_glm_max_d() { return 512; }
 
+// steps one launch of the regression step kernel may fuse (0: any): the single-slice MALA kernel is a
+// one-step kernel (glm_mala1)
+int mcmc_glm_steps_per_launch(int d, int64_t n, int sampler_kind) {
+    const mcmc::GlmShape g = mcmc_glm_shape(d, n);
+    return (g.nw == 1 && sampler_kind == mcmc::SK_MALA) ? 1 : 0;
+}
+
 int mcmc_glm_d_pad(int d) { return mcmc_glm_shape(d, 1).d_pad; }
 
 template <int NM, int NW>
@@ -1025,7 +1167,10 @@ static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hip
     constexpr int B = glm_block<NW>();
     switch (a.sa.kind) {
         case SK_RWM: glm_rwm<NM, NW><<<grid, B, lds, st>>>(a); break;
-        case SK_MALA: glm_mala<NM, NW><<<grid, B, lds, st>>>(a); break;
+        case SK_MALA:
+            if constexpr (NW == 1) glm_mala1<NM><<<grid, B, lds, st>>>(a);
+            else glm_mala<NM, NW><<<grid, B, lds, st>>>(a);
+            break;
         case SK_HMC: glm_hmc<NM, NW, false><<<grid, B, lds, st>>>(a); break;
         case SK_HMCDA: glm_hmc<NM, NW, true><<<grid, B, lds, st>>>(a); break;
         case SK_RAM:
