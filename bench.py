@@ -136,15 +136,19 @@ def kernel_name(cfg, d, sampler):
     return f"{'lpc' if d <= 32 else 'wpc'}_{sampler}"
 
 
-def measured_traffic(wkey):
+def measured_traffic(wkey, kname):
     """HBM bytes per launch of the step kernel for this workload: 2 x FETCH_SIZE + WRITE_SIZE of the timed
-    dispatch in a committed rocprofv3 run of the same bench command (MI355X_MICROARCH.md §HBM correction),
-    or None when no profile of this exact workload is committed."""
+    dispatch(es) in a committed rocprofv3 run of the same bench command (MI355X_MICROARCH.md §HBM correction),
+    or None when no profile of this exact workload and this kernel is committed (a profile of an earlier
+    kernel for the same workload is stale and is not used)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
     e = json.load(open(p)).get(wkey)
     if e is None:
+        return None
+    want = "mcmc::" + kname.replace(",DA", ",true").rstrip(">")     # e.g. mcmc::glm_hmc<4,8,true
+    if want not in e["kernel"].replace(" ", ""):
         return None
     return {"bytes_per_launch": e["traffic_bytes"], "read_bytes": e["read_bytes"], "write_bytes": e["write_bytes"],
             "source": e["source"], "unit": "B"}
@@ -311,10 +315,10 @@ def main():
     # per-GPU workload key: the PMC traffic of a committed rocprofv3 run of this same workload
     # (profiles/traffic.json, written by scripts/summarize_prof.py) fills roofline.traffic
     wkey = f"{args.config}|d={d}|chains={C}|{args.sampler}|steps={K}|thinning={args.thinning}|spl={spl}"
-    tdet = measured_traffic(wkey)
+    kname = kernel_name(cfg0, d, args.sampler)
+    tdet = measured_traffic(wkey, kname)
     traffic = tdet["bytes_per_launch"] if tdet else None
     avg_launch_s = kernel_ms * 1e-3 / launches          # HIP events around the launches, on their stream
-    kname = kernel_name(cfg0, d, args.sampler)
     if cfg0["model"] == "iso":
         per_step, per_kept = hbm_bytes_per_unit(d, args.sampler)
         nbytes = C * K * per_step + C * nkept * per_kept               # per run = per launch x launches

@@ -87,12 +87,18 @@ if step:
         per.append({"duration_us": dur, "read_bytes": rd, "write_bytes": wr})
         lines.append(f"| {i} | {r['Dispatch_Id']} | {dur:.1f} | {rd / 1e9 if rd is not None else float('nan'):.4f} | "
                      f"{wr / 1e9 if wr is not None else float('nan'):.4f} | {bw:.1f} |")
-    timed = per[-1]
-    lines += ["", "The timed launch is the last dispatch (the ones before it are the bench's warmup)."]
+    # the timed launches are the last `launches` dispatches (the ones before them are the bench's warmup);
+    # traffic and duration are their per-launch means
+    nt = max(1, int((bl or {}).get("roofline", {}).get("launches", 1)))
+    tl = per[-nt:]
+    mean = lambda k: (sum(t[k] for t in tl) / len(tl)) if all(t[k] is not None for t in tl) else None
+    timed = {k: mean(k) for k in ("duration_us", "read_bytes", "write_bytes")}
+    lines += ["", f"The timed launches are the last {nt} dispatch(es) (the ones before are the bench's warmup); "
+                  "the figures below are their per-launch means."]
     if bl is not None:
         roof = bl.get("roofline", {})
         lines.append(f"bench.py in the traced run: avg_launch_ms = {roof.get('avg_launch_ms', float('nan')):.3f} "
-                     f"(HIP events) vs {timed['duration_us'] / 1e3:.3f} ms for the last dispatch in the trace; "
+                     f"(HIP events) vs {timed['duration_us'] / 1e3:.3f} ms per timed dispatch in the trace; "
                      f"value = {bl['value']:.4g} {bl['unit']}.")
         key = bl.get("config", {}).get("key")
         if key and timed["read_bytes"] is not None and timed["write_bytes"] is not None:
