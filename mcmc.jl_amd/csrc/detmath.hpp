@@ -246,6 +246,105 @@ __device__ __forceinline__ double bm_log_u32(uint32_t w, const double (*tab)[4] 
     return hi + lo;
 }
 
+typedef double dm_f64x2 __attribute__((ext_vector_type(2)));
+
+// exp for the logistic likelihood (prob = 1/(1+exp(-X*vars)), examples/logistic_regression.jl:19), table-
+// driven: x = (64 E + j) ln2/64 + r with |r| <= ln2/128, exp(x) = 2^E (T_hi + (T_hi expm1(r) + T_lo)), where
+// (T_hi, T_lo) = 2^(j/64) (EXP2_TABLE_ROWS) and expm1(r) is Taylor to degree 6 (truncation < 2^-66 relative).
+// The argument is clamped to [-746, 710], so overflow and underflow come out of the 2^E scaling itself (inf,
+// 0); NaN passes through.  Stages as det_exp (the caller may interleave work between them); oracle twin
+// orc_exp_tab.  Against det_exp: a 6-term instead of a 13-term polynomial.
+static __device__ const double kExp2Tab[64][2] = {EXP2_TABLE_ROWS};
+
+struct ExpTState {
+    double x, r, em;
+    dm_f64x2 t;
+    int e;
+};
+__device__ __forceinline__ void det_exp_tab_s1(double x, ExpTState& E, const double (*tab)[2] = kExp2Tab) {
+    const double k64 = 0x1.71547652b82fep+6;                 // 64 / ln2
+    const double l_hi = 0x1.62e42fee00000p-7;                // ln2 / 64, high part (kd l_hi is exact)
+    const double l_lo = 0x1.a39ef35793c76p-39;               // ln2 / 64, low part
+    const double shifter = 0x1.8p52;
+    const double xc = __builtin_fmin(__builtin_fmax(x, -746.0), 710.0);
+    const double kd = __builtin_fma(xc, k64, shifter) - shifter;
+    const int k = (int)kd;
+    E.t = *reinterpret_cast<const dm_f64x2*>(tab[k & 63]);
+    E.e = k >> 6;                                            // floor(k / 64), in [-1077, 1024]
+    const double r = __builtin_fma(-kd, l_hi, xc);
+    E.r = __builtin_fma(-kd, l_lo, r);
+    E.x = x;
+}
+__device__ __forceinline__ void det_exp_tab_s2(ExpTState& E) {
+    const double r = E.r;
+    double P = __builtin_fma(r, 0x1.6c16c16c16c17p-10, 0x1.1111111111111p-7);   // 1/720, 1/120
+    P = __builtin_fma(r, P, 0x1.5555555555555p-5);                               // 1/24
+    P = __builtin_fma(r, P, 0x1.5555555555555p-3);                               // 1/6
+    P = __builtin_fma(r, P, 0.5);
+    P = __builtin_fma(r, P, 1.0);
+    E.em = r * P;                                                                // expm1(r)
+}
+__device__ __forceinline__ double det_exp_tab_fin(const ExpTState& E) {
+    const int e1 = E.e / 2, e2 = E.e - e1;
+    double res = E.t.x + __builtin_fma(E.t.x, E.em, E.t.y);
+    res = (res * pow2i(e1)) * pow2i(e2);
+    return E.x != E.x ? E.x : res;
+}
+__device__ __forceinline__ double det_exp_tab(double x, const double (*tab)[2] = kExp2Tab) {
+    ExpTState E;
+    det_exp_tab_s1(x, E, tab);
+    det_exp_tab_s2(E);
+    return det_exp_tab_fin(E);
+}
+
+// log of v in [0, 1] for the logistic Bernoulli term (logpdf(Bernoulli(prob), y) = log(prob) or log(1 - prob)):
+// bm_log_u32's table reduction applied to any double, v = 2^e m; a subnormal v is pre-scaled by 2^54 (a
+// select), log(0) = -inf, NaN passes through.  Division-free (det_log has one IEEE division); stages as
+// det_log; oracle twin orc_log_tab.  Not for negative or infinite v (unreachable: v = p or 1 - p, p in [0, 1]).
+struct LogTState {
+    double v, m, p;
+    dm_f64x2 a, t;
+    int e;
+};
+__device__ __forceinline__ void det_log_tab_s1(double v, LogTState& L, const double (*tab)[4] = kBmLogTab) {
+    const bool sub = v < 0x1p-1022;                                  // zero or subnormal
+    const double xs = sub ? v * 0x1p54 : v;
+    const uint64_t b = d2bits(xs);
+    const uint32_t top7 = (uint32_t)(b >> 45) & 0x7fu;
+    const uint32_t up = top7 >> 6;                                   // m in [1.5, 2): use m/2
+    L.e = (int)(uint32_t)(b >> 52) - 1023 + (int)up - (sub ? 54 : 0);
+    L.m = bits2d((b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52));
+    const dm_f64x2* row = reinterpret_cast<const dm_f64x2*>(tab[top7]);
+    L.a = row[0];                                                    // (inv_c, T_hi)
+    L.t = row[1];                                                    // (T_lo, 0)
+    L.v = v;
+}
+__device__ __forceinline__ void det_log_tab_s2(LogTState& L) {
+    const double r = __builtin_fma(L.m, L.a.x, -1.0);
+    double P = __builtin_fma(r, -0x1p-3, 0x1.2492492492492p-3);         // -1/8, 1/7
+    P = __builtin_fma(r, P, -0x1.5555555555555p-3);                     // -1/6
+    P = __builtin_fma(r, P, 0x1.999999999999ap-3);                      // 1/5
+    P = __builtin_fma(r, P, -0x1p-2);                                   // -1/4
+    P = __builtin_fma(r, P, 0x1.5555555555555p-2);                      // 1/3
+    P = __builtin_fma(r, P, -0x1p-1);                                   // -1/2
+    L.p = __builtin_fma(r * r, P, r);                                   // log1p(r)
+}
+__device__ __forceinline__ double det_log_tab_fin(const LogTState& L) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    const double de = (double)L.e;
+    const double hi = __builtin_fma(de, ln2_hi, L.a.y);
+    const double lo = __builtin_fma(de, ln2_lo, L.t.x) + L.p;
+    const double res = L.v == 0.0 ? -__builtin_inf() : hi + lo;
+    return L.v != L.v ? L.v : res;
+}
+__device__ __forceinline__ double det_log_tab(double v, const double (*tab)[4] = kBmLogTab) {
+    LogTState L;
+    det_log_tab_s1(v, L, tab);
+    det_log_tab_s2(L);
+    return det_log_tab_fin(L);
+}
+
 // sin, cos of 2 pi w 2^-32 (the Box-Muller angle), table-driven: the angle splits as k/256 + j 2^-32 turns
 // with k = (w + 2^23) >> 24 and |j| <= 2^23, so r = 2 pi j 2^-32 has |r| <= 2 pi 2^-9.  The row of k gives
 // (sin a, cos a) (scripts/gen_bm_log_table.py, full circle: no quadrant selects); sin r and cos r - 1 by

@@ -35,6 +35,12 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <int NW>
 constexpr int glm_block() { return 64 * (NW > 4 ? NW : 4); }
 constexpr int kGlmMaxWaves = 8;
+// glm_eval1's elementwise schedule (the same operations either way): each sub-stage between
+// eta MFMAs runs one stage of one observation row (0) or of all four rows of the lane (1)
+#ifndef GLM_GROUP_ROWS
+#define GLM_GROUP_ROWS 1
+#endif
+constexpr bool kGlmGroupRows = GLM_GROUP_ROWS != 0;
 // NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
 
 struct GlmShape {
@@ -251,12 +257,21 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         load_tile(1);
         store_tile(1);
     }
+    // logistic: the exp / log tables (det_exp_tab, det_log_tab) staged in the eta-partials area, which the
+    // single-slice kernels do not otherwise use
+    const double (*ltab)[4] = reinterpret_cast<const double (*)[4]>(L.part);
+    const double (*etab)[2] = reinterpret_cast<const double (*)[2]>(L.part + 4 * 128);
+    if (LOGI) {
+        for (int i = threadIdx.x; i < 4 * 128 + 2 * 64; i += kBlk)
+            L.part[i] = i < 4 * 128 ? (&kBmLogTab[0][0])[i] : (&kExp2Tab[0][0])[i - 4 * 128];
+    }
     if (GRAD) {
 #pragma unroll
         for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
     }
     __syncthreads();
     f64x4 eta = eta_of(0);
+    const int64_t nfull = M.n / 16;                           // tiles without padded observations
     int b = 0;                                                // buffer of tile t
     for (int64_t t = 0; t < ntiles; ++t) {
         const bool more = t + 2 < ntiles;
@@ -276,47 +291,57 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         double av[KM];
 #pragma unroll
         for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow1[16 * (m >> 2) + (m & 3)];
-        double y[4], ea[4], pr[4], term[4], rv[4];
-        ExpState E[4];
-        LogState Lg[4];
+        double y[4], pr[4], term[4], rv[4];
+        ExpTState E[4];
+        LogTState Lg[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
-        constexpr int NSTAGE = LOGI ? 8 : 1;
+        // sub-stage j: the eta MFMAs [j KM / NSUB, (j+1) KM / NSUB), then stage st of one row (kGlmGroupRows
+        // false) or of all four rows, four independent dependency chains (kGlmGroupRows true)
+        constexpr int NSTAGE = LOGI ? 6 : 1;
+        constexpr int NSUB = kGlmGroupRows ? NSTAGE : 4 * NSTAGE;
 #pragma unroll
-        for (int j = 0; j < 4 * NSTAGE; ++j) {
-            const int st = j >> 2, r = j & 3;
+        for (int j = 0; j < NSUB; ++j) {
 #pragma unroll
-            for (int m = j * KM / (4 * NSTAGE); m < (j + 1) * KM / (4 * NSTAGE); ++m) {
+            for (int m = j * KM / NSUB; m < (j + 1) * KM / NSUB; ++m) {
                 if (m + kLA < KM) av[m + kLA] = xrow1[16 * ((m + kLA) >> 2) + ((m + kLA) & 3)];
                 eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x(m), eta_next, 0, 0, 0);
             }
-            if (LOGI) {
-                switch (st) {
-                    case 0: det_exp_s1(-(sgn * eta[r]), E[r]); break;               // prob = 1/(1+exp(-X*vars))
-                    case 1: det_exp_s2(E[r]); break;
-                    case 2: det_exp_s3(E[r]); break;
-                    case 3: ea[r] = det_exp_fin(E[r]); pr[r] = 1.0 / (1.0 + ea[r]); break;
-                    case 4: det_log_s1((y[r] >= 0.5) ? pr[r] : 1.0 - pr[r], Lg[r]); break;   // Y ~ Bernoulli(prob)
-                    case 5: det_log_s2(Lg[r]); break;
-                    case 6: det_log_s3(Lg[r]); break;
-                    default:
-                        term[r] = det_log_fin(Lg[r]);
-                        rv[r] = sgn * (y[r] - pr[r]);                           // MCMCDerivRules.jl:111, closed form
-                        break;
+            const int st = kGlmGroupRows ? j : j >> 2;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (!kGlmGroupRows && r != (j & 3)) continue;
+                if (LOGI) {
+                    switch (st) {
+                        case 0: det_exp_tab_s1(-(sgn * eta[r]), E[r], etab); break;     // prob = 1/(1+exp(-X*vars))
+                        case 1: det_exp_tab_s2(E[r]); break;
+                        case 2: pr[r] = 1.0 / (1.0 + det_exp_tab_fin(E[r])); break;
+                        case 3: det_log_tab_s1((y[r] >= 0.5) ? pr[r] : 1.0 - pr[r], Lg[r], ltab); break;  // Y ~ Bernoulli
+                        case 4: det_log_tab_s2(Lg[r]); break;
+                        default:
+                            term[r] = det_log_tab_fin(Lg[r]);
+                            rv[r] = sgn * (y[r] - pr[r]);                           // MCMCDerivRules.jl:111, closed form
+                            break;
+                    }
+                } else {
+                    const double resid = y[r] - eta[r];                             // resid = Y - X*vars
+                    const double z = resid * isn;
+                    term[r] = -0.5 * (z * z + kLog2Pi) - logsn;                     // resid ~ Normal(0, sn)
+                    rv[r] = resid * is2n;
                 }
-            } else {
-                const double resid = y[r] - eta[r];                             // resid = Y - X*vars
-                const double z = resid * isn;
-                term[r] = -0.5 * (z * z + kLog2Pi) - logsn;                     // resid ~ Normal(0, sn)
-                rv[r] = resid * is2n;
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        if (t < nfull) {                                                        // uniform: no padded observation
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {                                           // the lane's terms in (t, r) order
-            const bool in = t * 16 + p.q + 4 * r < M.n;
-            lik_part = in ? lik_part + term[r] : lik_part;
-            rv[r] = in ? rv[r] : 0.0;
+            for (int r = 0; r < 4; ++r) lik_part = lik_part + term[r];          // the lane's terms in (t, r) order
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool in = t * 16 + p.q + 4 * r < M.n;
+                lik_part = in ? lik_part + term[r] : lik_part;
+                rv[r] = in ? rv[r] : 0.0;
+            }
         }
         if (GRAD) {
             // G tile T, k-slice kk: A[i][k] = X[obs 4kk+q][coord 16T+4(i&3)+(i>>2)], i = cl; kk outer so that
@@ -455,9 +480,9 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             const double y = LY[p.q + 4 * r];
             double term, w;
             if (logistic) {
-                const double tt = det_exp(-(sgn * e));                  // prob = 1/(1+exp(-X*vars))
+                const double tt = det_exp_tab(-(sgn * e));              // prob = 1/(1+exp(-X*vars))
                 const double pr = 1.0 / (1.0 + tt);
-                term = (y >= 0.5) ? det_log(pr) : det_log(1.0 - pr);   // Y ~ Bernoulli(prob)
+                term = det_log_tab((y >= 0.5) ? pr : 1.0 - pr);         // Y ~ Bernoulli(prob)
                 w = sgn * (y - pr);                                     // MCMCDerivRules.jl:111 chain, closed form
             } else {
                 const double resid = y - e;                             // resid = Y - X*vars

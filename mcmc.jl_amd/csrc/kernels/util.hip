@@ -79,6 +79,8 @@ __global__ void k_detmath(int op, int64_t n, const double* x, const double* y, d
         case 10: { double s, c; det_sincos2pi_u32((uint32_t)(uint64_t)a, s, c); r = s; } break;
         case 11: { double s, c; det_sincos2pi_u32((uint32_t)(uint64_t)a, s, c); r = c; } break;
         case 12: r = sqrt_pos_normal(a); break;
+        case 13: r = det_exp_tab(a); break;
+        case 14: r = det_log_tab(a); break;
         default: r = 0.0;
     }
     out[i] = r;

@@ -219,6 +219,65 @@ static inline double orc_bm_log_u32(uint32_t w) {
     return hi + lo;
 }
 
+/* ------------------------------------------------------- logistic-likelihood exp and log */
+/* exp for the logistic likelihood: x = (64 E + j) ln2/64 + r, |r| <= ln2/128; exp(x) = 2^E (T_hi + (T_hi
+   expm1(r) + T_lo)), (T_hi, T_lo) = 2^(j/64) from the generated table, expm1 by Taylor to degree 6.  x is
+   clamped to [-746, 710]: overflow / underflow come out of the 2^E scaling; NaN passes.  Device twin:
+   det_exp_tab (csrc/detmath.hpp). */
+static const double orc_exp2_tab[64][2] = {EXP2_TABLE_ROWS};
+
+static inline double orc_exp_tab(double x) {
+    const double k64 = 0x1.71547652b82fep+6;
+    const double l_hi = 0x1.62e42fee00000p-7;
+    const double l_lo = 0x1.a39ef35793c76p-39;
+    const double shifter = 0x1.8p52;
+    double xc = fmin(fmax(x, -746.0), 710.0);
+    double kd = fma(xc, k64, shifter) - shifter;
+    int k = (int)kd;
+    const double* t = orc_exp2_tab[k & 63];
+    int e = k >> 6;                                        /* floor(k / 64): arithmetic shift */
+    double r = fma(-kd, l_hi, xc);
+    r = fma(-kd, l_lo, r);
+    double P = fma(r, 0x1.6c16c16c16c17p-10, 0x1.1111111111111p-7);
+    P = fma(r, P, 0x1.5555555555555p-5);
+    P = fma(r, P, 0x1.5555555555555p-3);
+    P = fma(r, P, 0.5);
+    P = fma(r, P, 1.0);
+    double em = r * P;
+    int e1 = e / 2, e2 = e - e1;
+    double res = t[0] + fma(t[0], em, t[1]);
+    res = (res * orc_pow2i(e1)) * orc_pow2i(e2);
+    return x != x ? x : res;
+}
+
+/* log of v in [0, 1] (the logistic Bernoulli term): orc_bm_log_u32's table reduction for any double; subnormal
+   v pre-scaled by 2^54, log(0) = -inf, NaN passes.  Device twin: det_log_tab. */
+static inline double orc_log_tab(double v) {
+    const double ln2_hi = 0x1.62e42fee00000p-1;
+    const double ln2_lo = 0x1.a39ef35793c76p-33;
+    int sub = v < 0x1p-1022;
+    double xs = sub ? v * 0x1p54 : v;
+    uint64_t b = orc_d2bits(xs);
+    uint32_t top7 = (uint32_t)(b >> 45) & 0x7fu;
+    uint32_t up = top7 >> 6;
+    int e = (int)(uint32_t)(b >> 52) - 1023 + (int)up - (sub ? 54 : 0);
+    double m = orc_bits2d((b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52));
+    const double* row = orc_bm_log_tab[top7];
+    double r = fma(m, row[0], -1.0);
+    double P = fma(r, -0x1p-3, 0x1.2492492492492p-3);
+    P = fma(r, P, -0x1.5555555555555p-3);
+    P = fma(r, P, 0x1.999999999999ap-3);
+    P = fma(r, P, -0x1p-2);
+    P = fma(r, P, 0x1.5555555555555p-2);
+    P = fma(r, P, -0x1p-1);
+    double p = fma(r * r, P, r);
+    double de = (double)e;
+    double hi = fma(de, ln2_hi, row[1]);
+    double lo = fma(de, ln2_lo, row[2]) + p;
+    double res = v == 0.0 ? -INFINITY : hi + lo;
+    return v != v ? v : res;
+}
+
 /* ------------------------------------------------------- Box-Muller angle */
 /* sin, cos of 2 pi w 2^-32: angle = k/256 + j 2^-32 turns, k = (w + 2^23) >> 24, |j| <= 2^23; the row of k
    holds RN(sin, cos of 2 pi k/256) (scripts/gen_bm_log_table.py); r = 2 pi j 2^-32 (|r| <= 2 pi 2^-9),

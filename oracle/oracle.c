@@ -229,9 +229,9 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
                 term = -0.5 * (z * z + ORC_LOG2PI) - logsn;       /* resid ~ Normal(0, sn) */
                 r = resid * is2n;                                 /* -d/dresid, MCMCDerivRules.jl:57 */
             } else {
-                double tt = orc_exp(-(sgn * eta));                /* prob = 1/(1+exp(-X*vars)) */
+                double tt = orc_exp_tab(-(sgn * eta));            /* prob = 1/(1+exp(-X*vars)) */
                 double p = 1.0 / (1.0 + tt);
-                term = (y >= 0.5) ? orc_log(p) : orc_log(1.0 - p);   /* Y ~ Bernoulli(prob) */
+                term = orc_log_tab((y >= 0.5) ? p : 1.0 - p);     /* Y ~ Bernoulli(prob) */
                 /* d/deta of the Bernoulli term: the rule dd1 += 1/(p - 1 + y) (MCMCDerivRules.jl:111) times
                    dprob/deta = s t / (1+t)^2 is s (y - p) for y in {0, 1}; the closed form is used */
                 r = sgn * (y - p);
@@ -739,6 +739,8 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
             case 10: orc_sincos2pi_u32((uint32_t)(uint64_t)a, &sn, &cs); r = sn; break;
             case 11: orc_sincos2pi_u32((uint32_t)(uint64_t)a, &sn, &cs); r = cs; break;
             case 12: r = sqrt(a); break;     /* device: sqrt_pos_normal (guard-free IEEE sequence) */
+            case 13: r = orc_exp_tab(a); break;
+            case 14: r = orc_log_tab(a); break;
             case 8: {
                 uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
                 uint32_t key[2] = {0u, 0u}, w[4];

@@ -52,7 +52,8 @@ def _dev_math(op, x, y=None):
 
 @pytest.mark.parametrize("op,name", [(0, "log"), (1, "exp"), (2, "sin2pi"), (3, "cos2pi"), (4, "sqrt"),
                                      (5, "div"), (7, "round"), (9, "bm_log_u32"), (10, "sin2pi_u32"),
-                                     (11, "cos2pi_u32"), (12, "sqrt_pos_normal")])
+                                     (11, "cos2pi_u32"), (12, "sqrt_pos_normal"), (13, "exp_tab"),
+                                     (14, "log_tab")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -72,6 +73,13 @@ def test_device_detmath_bitwise(gpu, op, name):
         x = np.concatenate([np.floor(rng.uniform(0, 2**32, 200000)), np.arange(0, 2000),
                             2.0**32 - 1 - np.arange(0, 2000), (np.arange(-40, 40) + 2**29 * np.arange(1, 8)[:, None]
                                                                ).ravel() % 2**32])
+    elif op == 13:
+        x = np.concatenate([rng.uniform(-750, 712, 200000), rng.uniform(-40, 40, 200000),
+                            [0.0, np.inf, -np.inf, np.nan, 710.0, -746.0, -745.2, 709.79]])
+    elif op == 14:
+        x = np.concatenate([np.exp(rng.uniform(-745, 0, 200000)), rng.uniform(0, 1, 200000),
+                            1 - np.exp(rng.uniform(-40, 0, 100000)), rng.uniform(5e-324, 2.3e-308, 20000),
+                            [0.0, 1.0, 5e-324, 2.2250738585072014e-308, np.nan]])
     elif op == 5:
         x = rng.normal(size=200000) * np.exp(rng.uniform(-300, 300, 200000))
     else:

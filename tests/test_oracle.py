@@ -84,6 +84,28 @@ def test_det_exp_accuracy():
     assert sp[0] == 1.0 and sp[1] == 0.0 and sp[2] == np.inf and np.isnan(sp[3]) and sp[4] == 0 and sp[5] == np.inf
 
 
+def test_exp_tab_accuracy():
+    """det_exp_tab (logistic likelihood; table-driven, degree-6 polynomial): <= 1 ulp over the normal range;
+    inf / 0 / NaN at the ends, as det_exp."""
+    rng = np.random.default_rng(13)
+    x = np.concatenate([rng.uniform(-708, 709.7, 200000), rng.uniform(-40, 40, 200000)])
+    assert _ulps(orc.detmath(13, x), np.exp(x)).max() <= 1.0
+    sp = orc.detmath(13, np.array([0.0, -1000.0, 1000.0, np.nan, -np.inf, np.inf, 710.0, -746.0]))
+    assert sp[0] == 1.0 and sp[1] == 0.0 and sp[2] == np.inf and np.isnan(sp[3]) and sp[4] == 0.0
+    assert sp[5] == np.inf and sp[6] == np.inf and sp[7] == 0.0
+
+
+def test_log_tab_accuracy():
+    """det_log_tab (logistic Bernoulli term; bm_log_u32's table for any double in [0, 1]): <= 1 ulp,
+    subnormals included; log(0) = -inf, log(1) = 0, NaN passes."""
+    rng = np.random.default_rng(14)
+    v = np.concatenate([np.exp(rng.uniform(-744, 0, 200000)), rng.uniform(0, 1, 200000),
+                        1 - np.exp(rng.uniform(-36, -1, 100000)), rng.uniform(5e-324, 2.2e-308, 20000)])
+    v = v[v > 0]
+    assert _ulps(orc.detmath(14, v), np.log(v)).max() <= 1.0
+    sp = orc.detmath(14, np.array([0.0, 1.0, np.nan, 0.5]))
+    assert sp[0] == -np.inf and sp[1] == 0.0 and np.isnan(sp[2]) and sp[3] == np.log(0.5)
+
 def test_det_sincos2pi_accuracy():
     rng = np.random.default_rng(2)
     u = np.floor(rng.uniform(0, 2**32, 100000)) * 2.0**-32
