@@ -41,6 +41,11 @@ constexpr int kGlmMaxWaves = 8;
 #define GLM_GROUP_ROWS 1
 #endif
 constexpr bool kGlmGroupRows = GLM_GROUP_ROWS != 0;
+// 1: a scheduling fence after every sub-stage keeps the eta MFMAs spread over the elementwise work
+#ifndef GLM_FENCE
+#define GLM_FENCE 1
+#endif
+constexpr bool kGlmFence = GLM_FENCE != 0;
 // NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
 
 struct GlmShape {
@@ -330,7 +335,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
                     rv[r] = resid * is2n;
                 }
             }
-            __builtin_amdgcn_sched_barrier(0);
+            if (kGlmFence) __builtin_amdgcn_sched_barrier(0);
         }
         if (t < nfull) {                                                        // uniform: no padded observation
 #pragma unroll
