@@ -41,11 +41,17 @@ constexpr int kGlmMaxWaves = 8;
 #define GLM_GROUP_ROWS 1
 #endif
 constexpr bool kGlmGroupRows = GLM_GROUP_ROWS != 0;
-// 1: a scheduling fence after every sub-stage keeps the eta MFMAs spread over the elementwise work
+// 1: a scheduling fence after every elementwise sub-stage pins the eta MFMAs between them; 0 (default) leaves
+// the interleaving to the compiler: config 3 runs 3.7 % faster without the fences
 #ifndef GLM_FENCE
-#define GLM_FENCE 1
+#define GLM_FENCE 0
 #endif
 constexpr bool kGlmFence = GLM_FENCE != 0;
+// 1 (default): a fence after each k-slice of the G = X^T r MFMAs (operands one k-slice ahead)
+#ifndef GLM_GFENCE
+#define GLM_GFENCE 1
+#endif
+constexpr bool kGlmGFence = GLM_GFENCE != 0;
 // NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
 
 struct GlmShape {
@@ -120,7 +126,7 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     return L;
 }
 
-size_t glm_lds_bytes(const GlmShape& g) {
+static size_t glm_lds_bytes(const GlmShape& g) {
     return (size_t)(glm_xbufs(g.nw) * 16 * g.lds_stride + glm_xbufs(g.nw) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
                     4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8;
 }
@@ -364,7 +370,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
                 }
 #pragma unroll
                 for (int T = 0; T < NM; ++T) G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[T], rv[kk], G[T], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
+                if (kGlmGFence) __builtin_amdgcn_sched_barrier(0);
                 if (kk < 3) {
 #pragma unroll
                     for (int T = 0; T < NM; ++T) ga[T] = gn[T];
@@ -396,7 +402,6 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     if constexpr (NW == 1) return glm_eval1<NM, GRAD>(a, p, L, XArr<4 * NM>{x}, G, oos);
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
-    const int d = M.d;
     const int S = g.lds_stride;
     const bool logistic = M.kind == MK_LOGISTIC;
     const double sgn = M.link_sign;
@@ -1157,6 +1162,23 @@ static unsigned glm_grid(int64_t C, const GlmShape& g) {
 
 }  // namespace mcmc
 
+#ifdef GLM_MALA1_UNIT
+// glm_mala1.hip: the single-slice MALA kernels only, in a translation unit built with machine LICM
+hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
+    using namespace mcmc;
+    constexpr int B = glm_block<1>();
+    switch (nm) {
+        case 1: glm_mala1<1><<<grid, B, lds, st>>>(a); break;
+        case 2: glm_mala1<2><<<grid, B, lds, st>>>(a); break;
+        case 4: glm_mala1<4><<<grid, B, lds, st>>>(a); break;
+        case 8: glm_mala1<8><<<grid, B, lds, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#else
+hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st);
+
 mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
     // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1);
     // 128 < d <= 512: NW = 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW.
@@ -1198,7 +1220,7 @@ static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hip
     switch (a.sa.kind) {
         case SK_RWM: glm_rwm<NM, NW><<<grid, B, lds, st>>>(a); break;
         case SK_MALA:
-            if constexpr (NW == 1) glm_mala1<NM><<<grid, B, lds, st>>>(a);
+            if constexpr (NW == 1) return mcmc_launch_glm_mala1(NM, a, lds, grid, st);   // glm_mala1.hip
             else glm_mala<NM, NW><<<grid, B, lds, st>>>(a);
             break;
         case SK_HMC: glm_hmc<NM, NW, false><<<grid, B, lds, st>>>(a); break;
@@ -1249,3 +1271,4 @@ hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& k, const double* xin, do
     }
     return hipGetLastError();
 }
+#endif  // GLM_MALA1_UNIT
