@@ -1,0 +1,318 @@
+"""The oracle (oracle/oracle.c) against literal transcriptions of the reference samplers (CPU).
+
+The generators below follow their Julia sources statement by statement -- RWM.jl:43-72, MALA.jl:65-126
+(with EmpiricalMALATune, :19-43), HMC.jl:81-175 (leapfrog :93-102, EmpiricalHMCTune :20-47), HMCDA.jl:51-143
+and SerialMC.jl:37-85 -- using numpy vectors and libm math (math.log / exp / sqrt, numpy dot), and
+Julia's variable names.  Where Julia calls randn / rand they draw from the build's stream instead of dSFMT
+(DESIGN.md §3): Philox4x32-10 blocks (counter = chain, step, block, tag; key = seed) and the Box-Muller
+transform, here evaluated with libm.  The oracle computes the same algorithm with its own operation order
+and table-driven transcendentals (<= 1-2 ulp apart), so the kept samples agree to ~1e-13 and every accept
+decision agrees exactly.  This pins the restatement to the reference's control flow: the short-circuit
+RWM/MALA accept, MALA's proposal densities, the leapfrog order, HMC's always-drawn uniform, the tuners'
+adaptation schedule, HMCDA's NaN-initialised step (eps0 = 1, mu = log 10), its dual averaging while
+i < burnin, Julia-0.2 round, and SerialMC's kept range.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import mcmchip as mc
+import oracle_ref as orc
+
+RTOL = 1e-9
+
+
+# ------------------------------------------------------------------ the build's random stream
+def _block(seed, chain, step, block, tag):
+    ctr = np.array([[chain, step, block, tag]], dtype=np.uint32)
+    key = np.array([[seed & 0xFFFFFFFF, seed >> 32]], dtype=np.uint32)
+    return [int(v) for v in orc.philox(ctr, key)[0]]
+
+
+def randn(seed, chain, step, d):
+    """randn(d): Box-Muller pairs from blocks (chain, step, b, NORMAL=0), coordinate j = 4b + e."""
+    z = []
+    for b in range((d + 3) // 4):
+        w = _block(seed, chain, step, b, 0)
+        for k in (0, 2):
+            rad = math.sqrt(-2.0 * math.log((w[k] + 0.5) * 2.0**-32))
+            ang = 2.0 * math.pi * (w[k + 1] * 2.0**-32)
+            z += [rad * math.cos(ang), rad * math.sin(ang)]
+    return np.array(z[:d])
+
+
+def rand(seed, chain, step):
+    """rand(): a 53-bit uniform from block (chain, step, 0, ACCEPT=1)."""
+    w = _block(seed, chain, step, 0, 1)
+    return float(((w[0] >> 5) << 26) | (w[1] >> 6)) * 2.0**-53
+
+
+def jexp(x):
+    return float(np.exp(np.float64(x)))          # Julia exp: inf on overflow, not an exception
+
+
+# ------------------------------------------------------------------ models (README.md:60-72)
+class IsoDot:
+    """model(v -> -dot(v,v), grad = v -> -2v, init, scale)   (README.md:60,63; likmodel.jl:100-143)"""
+
+    def __init__(self, init, scale):
+        self.init, self.scale = np.asarray(init, float), np.asarray(scale, float)
+
+    def eval(self, v):
+        return -float(np.dot(v, v))
+
+    def evalallg(self, v):
+        return self.eval(v), -2.0 * v
+
+
+class NormalDSL:
+    """v ~ Normal(mu, sigma) through the DSL: LLAcc sums logpdf terms, a non-finite running sum gives
+    (-Inf, zeros) (AccumulatorDerivRules.jl:12-20, modelparser.jl:64-72); d/dv = (mu - v)/sigma^2
+    (MCMCDerivRules.jl:57-59)."""
+
+    def __init__(self, mu, sigma, init):
+        self.mu, self.sigma = mu, sigma
+        self.init = np.asarray(init, float)
+        self.scale = np.ones(len(self.init))
+
+    def eval(self, v):
+        acc = 0.0
+        for x in v:
+            z = (x - self.mu) / self.sigma
+            acc += -0.5 * (z * z + math.log(2 * math.pi)) - math.log(self.sigma)
+            if not math.isfinite(acc):
+                return -math.inf
+        return acc
+
+    def evalallg(self, v):
+        lp = self.eval(v)
+        if not math.isfinite(lp):
+            return -math.inf, np.zeros(len(v))
+        return lp, (self.mu - v) / self.sigma**2
+
+
+# ------------------------------------------------------------------ samplers (yield MCMCSample.ppars, pgrads, accept)
+def rwm_task(model, s, burnin, seed, chain):
+    """RWM.jl:43-72"""
+    scale = model.scale * s.scale                                   # model.scale .* sampler.scale
+    pars = model.init.copy()
+    logTarget = model.eval(pars)
+    assert math.isfinite(logTarget)
+    i = 0
+    while True:
+        i += 1
+        proposedPars = pars + randn(seed, chain, i, len(pars)) * scale
+        proposedLogTarget = model.eval(proposedPars)
+        ratio = proposedLogTarget - logTarget
+        if ratio > 0 or (ratio > math.log(rand(seed, chain, i))):
+            yield proposedPars, None, True
+            pars, logTarget = proposedPars.copy(), proposedLogTarget
+        else:
+            yield pars, None, False
+
+
+def mala_task(model, s, burnin, seed, chain):
+    """MALA.jl:65-126 (EmpiricalMALATune / adapt!: MALA.jl:19-43)"""
+    pars = model.init.copy()
+    logTarget, grad = model.evalallg(pars)
+    tune = {"driftStep": s.driftStep, "accepted": 0, "proposed": 0} if s.tuner is not None else None
+    i = 1
+    while True:
+        if tune is not None:
+            tune["proposed"] += 1
+            driftStep = tune["driftStep"]
+        else:
+            driftStep = s.driftStep
+        parsMean = pars + (driftStep / 2.0) * grad
+        proposedPars = parsMean + math.sqrt(driftStep) * randn(seed, chain, i, len(pars))
+        proposedLogTarget, proposedGrad = model.evalallg(proposedPars)
+        probNewGivenOld = np.sum(-(parsMean - proposedPars) ** 2 / (2 * driftStep) - math.log(2 * math.pi * driftStep) / 2)
+        parsMean = proposedPars + (driftStep / 2) * proposedGrad
+        probOldGivenNew = np.sum(-(parsMean - pars) ** 2 / (2 * driftStep) - math.log(2 * math.pi * driftStep) / 2)
+        ratio = proposedLogTarget + probOldGivenNew - logTarget - probNewGivenOld
+        if ratio > 0 or (ratio > math.log(rand(seed, chain, i))):
+            yield proposedPars, proposedGrad, True
+            pars, logTarget, grad = proposedPars.copy(), proposedLogTarget, proposedGrad.copy()
+            if tune is not None:
+                tune["accepted"] += 1
+        else:
+            yield pars, grad, False
+        if tune is not None and i <= burnin and i % s.tuner.adaptStep == 0:
+            rate = tune["accepted"] / tune["proposed"]
+            tune["driftStep"] *= (1 / (1 + jexp(-11 * (rate - s.tuner.targetRate))) + 0.5)
+            tune["accepted"], tune["proposed"] = 0, 0
+        i += 1
+
+
+class HMCSample:
+    """HMC.jl:81-91; HMCSample(pars) has H = NaN until update!"""
+
+    def __init__(self, pars, grad=None, m=None, logTarget=math.nan, H=math.nan):
+        self.pars, self.grad, self.m, self.logTarget, self.H = pars, grad, m, logTarget, H
+
+    def copy(self):
+        return HMCSample(self.pars.copy(), None if self.grad is None else self.grad.copy(),
+                         None if self.m is None else self.m.copy(), self.logTarget, self.H)
+
+    def calc(self, model):
+        self.logTarget, self.grad = model.evalallg(self.pars)
+
+    def update(self):
+        self.H = -self.logTarget + 0.5 * float(np.dot(self.m, self.m))
+
+
+def leapfrog(s, ve, model):
+    """HMC.jl:93-102"""
+    n = s.copy()
+    n.m = n.m + 0.5 * n.grad * ve
+    n.pars = n.pars + ve * n.m
+    n.calc(model)
+    n.m = n.m + 0.5 * n.grad * ve
+    n.update()
+    return n
+
+
+def hmc_task(model, s, burnin, seed, chain):
+    """HMC.jl:106-175 (EmpiricalHMCTune / adapt!: HMC.jl:20-47)"""
+    state0 = HMCSample(model.init.copy())
+    state0.calc(model)
+    tune = ({"nLeaps": s.nLeaps, "leapStep": s.leapStep, "accepted": 0, "proposed": 0}
+            if s.tuner is not None else None)
+    i = 1.0                                                          # for i in 1:Inf
+    while True:
+        if tune is not None:
+            tune["proposed"] += 1
+            nLeaps, leapStep = tune["nLeaps"], tune["leapStep"]
+        else:
+            nLeaps, leapStep = s.nLeaps, s.leapStep
+        state0.m = randn(seed, chain, int(i), len(state0.pars))
+        state0.update()
+        state = state0.copy()
+        for _ in range(int(nLeaps)):
+            state = leapfrog(state, leapStep, model)
+        if rand(seed, chain, int(i)) < jexp(state0.H - state.H):
+            yield state.pars, state.grad, True
+            state0 = state.copy()
+            if tune is not None:
+                tune["accepted"] += 1
+        else:
+            yield state0.pars, state0.grad, False
+        if tune is not None and i <= burnin and i % s.tuner.adaptStep == 0:
+            t = tune
+            t["rate"] = t["accepted"] / t["proposed"]
+            t["leapStep"] *= (1 / (1 + jexp(-11 * (t["rate"] - s.tuner.targetRate))) + 0.5)
+            t["nLeaps"] = min(s.tuner.maxStep, math.ceil(s.tuner.targetPath / t["leapStep"]))
+            t["accepted"], t["proposed"] = 0, 0
+        i += 1.0
+
+
+def julia02_round(x):
+    """Julia 0.2 round: ties away from zero"""
+    return math.floor(x + 0.5) if x >= 0 else -math.floor(-x + 0.5)
+
+
+def jmin(a, b):
+    """Julia 0.2 min(1, NaN) ignored the NaN (libm fmin)"""
+    return float(np.fmin(a, b))
+
+
+def hmcda_task(model, s, burnin, seed, chain):
+    """HMCDA.jl:72-143 with initializeHMCDAStep (:51-69)"""
+    state0 = HMCSample(model.init.copy())
+    state0.calc(model)
+    # state0.m = randn(model.size); leapStep = initializeHMCDAStep(model, state0): state0.H is still NaN
+    # (HMCSample ctor, update! not called), so p = exp(s.H - NaN) = NaN, a = -1, and the while test
+    # NaN^-1 > 2 is false: leapStep = 1 without moving
+    leapStep = 1.0
+    p = math.nan
+    a = 2 * (p > 0.5) - 1
+    assert not (p ** a > 2 ** (-a))
+    mu = math.log(10 * leapStep)
+    dualLeapStep = 1.0
+    dualH = 0.0
+    i = 1.0
+    while True:
+        state0.m = randn(seed, chain, int(i), len(state0.pars))
+        state0.update()
+        state = state0.copy()
+        nLeaps = max(1, julia02_round(s.len / leapStep))
+        for _ in range(int(nLeaps)):
+            state = leapfrog(state, leapStep, model)
+        p = jmin(1.0, jexp(state0.H - state.H))
+        if rand(seed, chain, int(i)) < p:
+            yield state.pars, state.grad, True
+            state0 = state.copy()
+        else:
+            yield state0.pars, state0.grad, False
+        if i < burnin:
+            eta = 1 / (i + s.t0)
+            dualH = (1 - eta) * dualH + eta * (s.rate - p)
+            leapStep = jexp(mu - math.sqrt(i) * dualH / s.shrinkage)
+            eta = i ** (-s.step)
+            dualLeapStep = jexp((1 - eta) * math.log(dualLeapStep) + eta * math.log(leapStep))
+        else:
+            leapStep = dualLeapStep
+        i += 1.0
+
+
+TASKS = {1: rwm_task, 2: mala_task, 3: hmc_task, 4: hmcda_task}
+
+
+def run_serialmc(task, steps, burnin, thinning):
+    """SerialMC.jl:37-85: consume `steps` samples, keep ppars (and pgrads) for i in (burnin+1):thinning:steps"""
+    r = range(burnin + 1, steps + 1, thinning)
+    kept, grads, acc = [], [], []
+    for i in range(1, steps + 1):
+        ppars, pgrads, accept = next(task)
+        if i in r:
+            kept.append(np.array(ppars, float))
+            grads.append(None if pgrads is None else np.array(pgrads, float))
+            acc.append(accept)
+    return kept, grads, acc
+
+
+SAMPLERS = {
+    "rwm": lambda: mc.RWM(0.6),
+    "mala": lambda: mc.MALA(0.4),
+    "mala_tuned": lambda: mc.MALA(2.0, mc.EmpMCTuner(0.6, adaptStep=7)),
+    "hmc": lambda: mc.HMC(4, 0.3),
+    "hmc_tuned": lambda: mc.HMC(3, 0.9, mc.EmpMCTuner(0.7, adaptStep=5, maxStep=9)),
+    "hmcda": lambda: mc.HMCDA(len=0.8),
+}
+
+
+def _models(kind, d):
+    init = np.linspace(0.5, 1.5, d)
+    if kind == "iso":
+        scale = np.linspace(0.8, 1.2, d)
+        return mc.model(mc.IsoNormalDot(), init=init, grad=True, scale=scale), IsoDot(init, scale)
+    return (mc.model(mc.NormalDSL(0.3, 1.7), v=init, gradient=True), NormalDSL(0.3, 1.7, init))
+
+
+@pytest.mark.parametrize("sname", list(SAMPLERS))
+@pytest.mark.parametrize("kind", ["iso", "normal"])
+@pytest.mark.parametrize("d", [3, 7])
+def test_oracle_matches_literal_reference(sname, kind, d):
+    steps, burnin, thinning, C, seed = 40, 12, 3, 12, 4242 + d
+    m, lit = _models(kind, d)
+    sp = SAMPLERS[sname]()
+    oc = orc.OracleChains(m, sp, nchains=C, seed=seed)
+    s_orc, g_orc, a_orc = oc.run(mc.SerialMC(steps=steps, burnin=burnin, thinning=thinning), nthreads=1)
+    for c in range(C):
+        kept, grads, acc = run_serialmc(TASKS[sp.kind](lit, sp, burnin, seed, c), steps, burnin, thinning)
+        assert list(a_orc[:, c].astype(bool)) == acc, f"chain {c}: accept decisions differ"
+        np.testing.assert_allclose(s_orc[:, :, c], np.array(kept), rtol=RTOL, atol=1e-12)
+        if g_orc is not None and grads[0] is not None:
+            np.testing.assert_allclose(g_orc[:, :, c], np.array(grads), rtol=RTOL, atol=1e-12)
+    if sname == "rwm":
+        assert 0 < a_orc.mean() < 1                                  # both branches of the short circuit
+
+
+def test_hmcda_initial_step_is_one_because_h_is_nan():
+    """HMCDA.jl:86-92 with HMC.jl:88: the first trajectory runs round(len / 1) leapfrogs."""
+    m, lit = _models("iso", 3)
+    sp = mc.HMCDA(len=3.4)
+    oc = orc.OracleChains(m, sp, nchains=1, seed=5)
+    oc.run(mc.SerialMC(steps=1, burnin=0, thinning=1), nthreads=1)
+    assert int(oc.n_evals[0]) == julia02_round(3.4 / 1.0) == 3
