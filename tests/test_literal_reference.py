@@ -316,3 +316,84 @@ def test_hmcda_initial_step_is_one_because_h_is_nan():
     oc = orc.OracleChains(m, sp, nchains=1, seed=5)
     oc.run(mc.SerialMC(steps=1, burnin=0, thinning=1), nthreads=1)
     assert int(oc.n_evals[0]) == julia02_round(3.4 / 1.0) == 3
+
+
+# ------------------------------------------------------------------ regression examples
+class LogisticExample:
+    """examples/logistic_regression.jl:16-22:  vars ~ Normal(0, 1.0); prob = 1 / (1. + exp(- X * vars));
+    Y ~ Bernoulli(prob).  LLAcc after each statement; d/dvars of the Bernoulli term in closed form X'(Y - prob)."""
+
+    def __init__(self, X, Y):
+        self.X, self.Y = X, Y
+        self.init = np.zeros(X.shape[1])
+        self.scale = np.ones(X.shape[1])
+
+    def evalallg(self, v):
+        acc = float(np.sum(-0.5 * (v * v + math.log(2 * math.pi)) - math.log(1.0)))
+        if not math.isfinite(acc):
+            return -math.inf, np.zeros(len(v))
+        prob = 1 / (1.0 + np.exp(-(self.X @ v)))
+        with np.errstate(divide="ignore"):
+            acc += float(np.sum(np.where(self.Y >= 0.5, np.log(prob), np.log(1 - prob))))
+        if not math.isfinite(acc):
+            return -math.inf, np.zeros(len(v))
+        return acc, -v + self.X.T @ (self.Y - prob)
+
+    def eval(self, v):
+        return self.evalallg(v)[0]
+
+
+class LinearExample:
+    """examples/linear_regression.jl:14-20:  vars ~ Normal(0, 1.0); resid = Y - X * vars; resid ~ Normal(0, 1.0)"""
+
+    def __init__(self, X, Y):
+        self.X, self.Y = X, Y
+        self.init = np.zeros(X.shape[1])
+        self.scale = np.ones(X.shape[1])
+
+    def evalallg(self, v):
+        acc = float(np.sum(-0.5 * (v * v + math.log(2 * math.pi))))
+        resid = self.Y - self.X @ v
+        acc += float(np.sum(-0.5 * (resid * resid + math.log(2 * math.pi))))
+        if not math.isfinite(acc):
+            return -math.inf, np.zeros(len(v))
+        return acc, -v + self.X.T @ resid
+
+    def eval(self, v):
+        return self.evalallg(v)[0]
+
+
+GLM_SAMPLERS = {
+    "rwm": lambda: mc.RWM(0.05),
+    "mala": lambda: mc.MALA(0.002),
+    "mala_tuned": lambda: mc.MALA(0.01, mc.EmpMCTuner(0.6, adaptStep=3)),
+    "hmc": lambda: mc.HMC(3, 0.02),
+    "hmc_tuned": lambda: mc.HMC(2, 0.05, mc.EmpMCTuner(0.7, adaptStep=3, maxStep=6)),
+    "hmcda": lambda: mc.HMCDA(len=0.1),
+}
+
+
+@pytest.mark.parametrize("sname", list(GLM_SAMPLERS))
+@pytest.mark.parametrize("kind", ["logistic", "linear"])
+def test_oracle_matches_literal_regression_examples(sname, kind):
+    d, n = 6, 40
+    i = np.arange(n)[:, None]
+    X = np.hstack([np.ones((n, 1)), np.sin(0.7 * i * np.arange(1, d)[None, :] + 0.3)])
+    eta = X @ (0.4 * np.cos(np.arange(d)))
+    if kind == "logistic":
+        Y = (np.cos(1.3 * np.arange(n)) * 0.5 + 0.5 < 1 / (1 + np.exp(-eta))).astype(float)
+        m, lit = mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(d), gradient=True), LogisticExample(X, Y)
+    else:
+        Y = eta + 0.5 * np.sin(2.1 * np.arange(n))
+        m, lit = (mc.model(mc.LinearRegression(X, Y, prior_sigma=1.0, noise_sigma=1.0), vars=np.zeros(d), gradient=True),
+                  LinearExample(X, Y))
+    steps, burnin, thinning, C, seed = 30, 12, 3, 8, 777
+    sp = GLM_SAMPLERS[sname]()
+    oc = orc.OracleChains(m, sp, nchains=C, seed=seed)
+    s_orc, g_orc, a_orc = oc.run(mc.SerialMC(steps=steps, burnin=burnin, thinning=thinning), nthreads=1)
+    for c in range(C):
+        kept, grads, acc = run_serialmc(TASKS[sp.kind](lit, sp, burnin, seed, c), steps, burnin, thinning)
+        assert list(a_orc[:, c].astype(bool)) == acc, f"chain {c}: accept decisions differ"
+        np.testing.assert_allclose(s_orc[:, :, c], np.array(kept), rtol=RTOL, atol=1e-12)
+        if g_orc is not None and grads[0] is not None:
+            np.testing.assert_allclose(g_orc[:, :, c], np.array(grads), rtol=1e-8, atol=1e-10)
