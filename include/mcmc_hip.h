@@ -199,6 +199,14 @@ int mcmc_chains_reserve_outputs(mcmc_chains* chains, int64_t nkept, int32_t on_d
  * bounded number of steps); for timing per launch. */
 int mcmc_chains_launches(mcmc_chains* chains, int64_t len, int64_t* launches);
 
+/* storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117; HMC and HMCDA only).  The next mcmc_run_serialmc records, for
+ * every kept step, the states of its trajectory -- leap 0 = state0 after update!, leap l = the state after
+ * the l-th leapfrog, l <= min(nLeaps, cap) -- into host buffers: pars, grads, mom [nkept][cap+1][d][C];
+ * lp, H [nkept][cap+1][C] (NaN past nLeaps); nleaps [nkept][C] (the full nLeaps, also when above cap).
+ * That run takes one step per launch.  pars == NULL switches it off; one run consumes the registration. */
+int mcmc_chains_store_leaps(mcmc_chains* chains, int64_t cap, double* pars, double* grads, double* mom, double* lp,
+                            double* H, int32_t* nleaps);
+
 /* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
 int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);
 

@@ -81,6 +81,18 @@ struct StepArgs {
     unsigned long long* n_evals;  // running count of log-target evaluations over all chains (NULL: off)
 };
 
+// storeLeaps record of one kept step (HMC.jl:145-150): device pointers already offset to that step;
+// pars / grads / mom [cap+1][d][C], lp / H [cap+1][C], nl [C]
+struct LeapRec {
+    int64_t cap;
+    double* pars;
+    double* grads;
+    double* mom;
+    double* lp;
+    double* H;
+    int32_t* nl;
+};
+
 __host__ __device__ inline bool kept_index(int64_t i_loc, int64_t burnin, int64_t thinning, int64_t len,
                                            int64_t* kk) {
     if (i_loc <= burnin || i_loc > len) return false;

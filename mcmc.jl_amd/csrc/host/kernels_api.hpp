@@ -26,6 +26,10 @@ hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, do
 int mcmc_wpc_max_d();
 // regression models on fp64 MFMA, state [d][ld] (+ gradient [d][ld])
 hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& a, hipStream_t st);
+// storeLeaps: record the trajectory of the next step (HMC / HMCDA) without moving the chains
+hipError_t mcmc_launch_lpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st);
+hipError_t mcmc_launch_wpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st);
+hipError_t mcmc_launch_glm_record(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st);
 hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_glm_max_d();

@@ -94,6 +94,11 @@ struct mcmc_chains {
     int64_t spl = 0;                 // steps per launch (0: whole run)
     int store_grads = 1;
     DevBuf out_samples, out_grads, out_bits, out_tmp, stage_samples, stage_grads;
+    // storeLeaps (HMC.jl:145-150): host buffers the next run fills (h_lpars == NULL: off), device staging
+    int64_t leap_cap = 0;
+    double *h_lpars = nullptr, *h_lgrads = nullptr, *h_lmom = nullptr, *h_llp = nullptr, *h_lH = nullptr;
+    int32_t* h_lnl = nullptr;
+    DevBuf leap_buf;
 };
 
 // Transfers are ordered on the context's (non-blocking) stream, after every kernel queued there,
@@ -453,6 +458,10 @@ static hipError_t launch_eval(Layout L, const KernelArgs& a, const double* xin, 
     return L == LAYOUT_LPC ? mcmc_launch_lpc_eval(a, xin, lp, g, check, st)
                            : mcmc_launch_wpc_eval(a, xin, lp, g, check, st);
 }
+static hipError_t launch_record(Layout L, const KernelArgs& a, const LeapRec& r, hipStream_t st) {
+    if (L == LAYOUT_GLM) return mcmc_launch_glm_record(a, r, st);
+    return L == LAYOUT_LPC ? mcmc_launch_lpc_record(a, r, st) : mcmc_launch_wpc_record(a, r, st);
+}
 static hipError_t launch_step(Layout L, const KernelArgs& a, hipStream_t st) {
     if (L == LAYOUT_GLM) return mcmc_launch_glm_step(a, st);
     return L == LAYOUT_LPC ? mcmc_launch_lpc_step(a, st) : mcmc_launch_wpc_step(a, st);
@@ -775,6 +784,27 @@ extern "C" int mcmc_chains_reserve_outputs(mcmc_chains* c, int64_t nkept, int32_
     return MCMC_OK;
 }
 
+extern "C" int mcmc_chains_store_leaps(mcmc_chains* c, int64_t cap, double* pars, double* grads, double* mom,
+                                       double* lp, double* H, int32_t* nleaps) {
+    if (!c) return fail(MCMC_E_INVALID_ARG, "NULL chains");
+    if (pars == nullptr) {
+        c->h_lpars = nullptr;
+        c->leap_cap = 0;
+        return MCMC_OK;
+    }
+    if (c->sa.kind != SK_HMC && c->sa.kind != SK_HMCDA)
+        return fail(MCMC_E_INVALID_ARG, "storeLeaps needs an HMC or HMCDA sampler");
+    if (cap < 0 || !grads || !mom || !lp || !H || !nleaps) return fail(MCMC_E_INVALID_ARG, "bad storeLeaps buffers");
+    c->leap_cap = cap;
+    c->h_lpars = pars;
+    c->h_lgrads = grads;
+    c->h_lmom = mom;
+    c->h_llp = lp;
+    c->h_lH = H;
+    c->h_lnl = nleaps;
+    return MCMC_OK;
+}
+
 // ------------------------------------------------------------------ run
 extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs* out) {
     if (!c || !r) return fail(MCMC_E_INVALID_ARG, "NULL argument");
@@ -858,7 +888,19 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     s.nw = nw;
     s.n_evals = c->d_evals;
 
-    const int64_t spl = launch_steps(c, r->len);
+    // storeLeaps: one step per launch; before each kept step, a record launch of its trajectory
+    const bool rec = c->h_lpars != nullptr;
+    const int64_t spl = rec ? 1 : launch_steps(c, r->len);
+    const size_t lsz = rec ? (size_t)(c->leap_cap + 1) * (size_t)d * (size_t)C : 0;   // doubles per kept step
+    const size_t lsc = rec ? (size_t)(c->leap_cap + 1) * (size_t)C : 0;
+    const size_t nk = (size_t)nkept;
+    double* dl = nullptr;
+    if (rec) {
+        if (int rc = ensure(c->leap_buf, nk * (3 * lsz + 2 * lsc) * 8 + nk * (size_t)C * 4)) return rc;
+        dl = (double*)c->leap_buf.p;
+        HIP_TRY(mcmc_fill_f64(dl, (int64_t)(nk * (3 * lsz + 2 * lsc)), __builtin_nan(""), st));
+        HIP_TRY(hipMemsetAsync(dl + nk * (3 * lsz + 2 * lsc), 0, nk * (size_t)C * 4, st));
+    }
     HIP_TRY(hipStreamSynchronize(st));
     auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventRecord(ctx->ev0, st));
@@ -867,6 +909,18 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
         const int64_t n = std::min(spl, r->len - done);
         s.step_begin = c->steps_done + done + 1;
         s.nsteps = (int32_t)n;
+        int64_t kk;
+        if (rec && kept_index(done + 1, r->burnin, r->thinning, r->len, &kk)) {
+            LeapRec lr;
+            lr.cap = c->leap_cap;
+            lr.pars = dl + (size_t)kk * lsz;
+            lr.grads = dl + nk * lsz + (size_t)kk * lsz;
+            lr.mom = dl + 2 * nk * lsz + (size_t)kk * lsz;
+            lr.lp = dl + 3 * nk * lsz + (size_t)kk * lsc;
+            lr.H = dl + 3 * nk * lsz + nk * lsc + (size_t)kk * lsc;
+            lr.nl = (int32_t*)(dl + 3 * nk * lsz + 2 * nk * lsc) + (size_t)kk * (size_t)C;
+            HIP_TRY(launch_record(L, a, lr, st));
+        }
         HIP_TRY(launch_step(L, a, st));
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
@@ -879,6 +933,15 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     c->steps_done += r->len;
+    if (rec) {
+        HIP_TRY(d2h(ctx, c->h_lpars, dl, nk * lsz * 8));
+        HIP_TRY(d2h(ctx, c->h_lgrads, dl + nk * lsz, nk * lsz * 8));
+        HIP_TRY(d2h(ctx, c->h_lmom, dl + 2 * nk * lsz, nk * lsz * 8));
+        HIP_TRY(d2h(ctx, c->h_llp, dl + 3 * nk * lsz, nk * lsc * 8));
+        HIP_TRY(d2h(ctx, c->h_lH, dl + 3 * nk * lsz + nk * lsc, nk * lsc * 8));
+        HIP_TRY(d2h(ctx, c->h_lnl, dl + 3 * nk * lsz + 2 * nk * lsc, nk * (size_t)C * 4));
+        c->h_lpars = nullptr;                          // one run consumes the registration
+    }
 
     if (out) {
         out->nkept = nkept;

@@ -70,6 +70,7 @@ struct GlmArgs {
     ModelArgs m;
     ChainState st;
     GlmShape g;
+    LeapRec rec;      // storeLeaps record (glm_hmc<..., REC = true>); zero otherwise
 };
 
 // lane position inside the workgroup
@@ -1018,7 +1019,22 @@ __global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
     glm_count_evals(a, p, s.nsteps);
 }
 
-template <int NM, int NW, bool DA>
+// storeLeaps: leap l's state into the record, [l][d][C] and [l][C] (HMC.jl:145-150)
+template <int NM>
+__device__ __forceinline__ void glm_rec_put(const GlmArgs& a, const GlmPos& p, int64_t l, const double (&x)[4 * NM],
+                                            const f64x4 (&g)[NM], const double (&m)[4 * NM], double lpv, double Hv) {
+    if (l > a.rec.cap) return;
+    glm_store_kept<NM>(a, p, l, a.rec.pars, x);
+    glm_store_kept4<NM>(a, p, l, a.rec.grads, g);
+    glm_store_kept<NM>(a, p, l, a.rec.mom, m);
+    if (p.live && p.q == 0 && p.slice == 0) {
+        a.rec.lp[(size_t)l * (size_t)a.s.C + (size_t)p.c] = lpv;
+        a.rec.H[(size_t)l * (size_t)a.s.C + (size_t)p.c] = Hv;
+    }
+}
+
+// REC: record the trajectory of the launch's single step (storeLeaps) and leave the chains where they are
+template <int NM, int NW, bool DA, bool REC = false>
 __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const StepArgs& s = a.s;
@@ -1052,6 +1068,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
         const double H0 = -lp + 0.5 * glm_sum(a, p, L, mm);         // update!(state0)
         glm_load<NM>(a, p, a.st.x, x);
         glm_load4<NM>(a, p, a.st.g, g);
+        if (REC) glm_rec_put<NM>(a, p, 0, x, g, m, lp, H0);             // leapStates[1] = deepcopy(state0)
         int64_t nl;
         if (DA) {
             const double r = round_away(sa.len / eps);              // HMCDA.jl:104
@@ -1077,6 +1094,18 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
 #pragma unroll
                 for (int slot = 0; slot < (4 * NM); ++slot) m[slot] = m[slot] + (0.5 * g[slot >> 2][slot & 3]) * eps;
             }
+            if (REC) {
+                double m2 = 0.0;
+#pragma unroll
+                for (int slot = 0; slot < (4 * NM); ++slot)
+                    if (glm_valid(a, p, slot)) m2 = __builtin_fma(m[slot], m[slot], m2);
+                const double Hl = -lpl + 0.5 * glm_sum(a, p, L, m2);      // update!(n): every wave reaches it
+                if (active) glm_rec_put<NM>(a, p, l + 1, x, g, m, lpl, Hl);
+            }
+        }
+        if (REC) {                                                       // uniform: every wave returns here
+            if (p.live && p.q == 0 && p.slice == 0) a.rec.nl[p.c] = (int32_t)nl;
+            return;
         }
         mm = 0.0;
 #pragma unroll
@@ -1152,6 +1181,7 @@ static GlmArgs glm_args(const KernelArgs& k, const GlmShape& g) {
     a.m = k.m;
     a.st = k.st;
     a.g = g;
+    a.rec = LeapRec{};
     return a;
 }
 
@@ -1249,6 +1279,34 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& k, hipStream_t st) {
         case 81: return glm_step_nm<8, 1>(a, lds, grid, st);
         case 44: return glm_step_nm<4, 4>(a, lds, grid, st);
         case 48: return glm_step_nm<4, 8>(a, lds, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int NM, int NW>
+static hipError_t glm_rec_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
+    using namespace mcmc;
+    constexpr int B = glm_block<NW>();
+    if (a.sa.kind == SK_HMCDA) glm_hmc<NM, NW, true, true><<<grid, B, lds, st>>>(a);
+    else glm_hmc<NM, NW, false, true><<<grid, B, lds, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t mcmc_launch_glm_record(const mcmc::KernelArgs& k, const mcmc::LeapRec& r, hipStream_t st) {
+    using namespace mcmc;
+    if (k.sa.kind != SK_HMC && k.sa.kind != SK_HMCDA) return hipErrorInvalidValue;
+    const GlmShape g = mcmc_glm_shape(k.s.d, k.m.n);
+    GlmArgs a = glm_args(k, g);
+    a.rec = r;
+    const size_t lds = glm_lds_bytes(g);
+    const dim3 grid(glm_grid(k.s.C, g));
+    switch (g.nm * 10 + g.nw) {
+        case 11: return glm_rec_nm<1, 1>(a, lds, grid, st);
+        case 21: return glm_rec_nm<2, 1>(a, lds, grid, st);
+        case 41: return glm_rec_nm<4, 1>(a, lds, grid, st);
+        case 81: return glm_rec_nm<8, 1>(a, lds, grid, st);
+        case 44: return glm_rec_nm<4, 4>(a, lds, grid, st);
+        case 48: return glm_rec_nm<4, 8>(a, lds, grid, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -6,7 +6,8 @@
 #define MCMC_LAYOUT_UNIT_DECL(prefix, name)                                                            \
     hipError_t mcmc_##prefix##_step_##name(const mcmc::KernelArgs& a, hipStream_t st);                \
     hipError_t mcmc_##prefix##_eval_##name(const mcmc::KernelArgs& a, const double* xin, double* lp,  \
-                                           double* g, int check, hipStream_t st);
+                                           double* g, int check, hipStream_t st);          \
+    hipError_t mcmc_##prefix##_record_##name(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st);
 MCMC_LAYOUT_UNIT_DECL(lpc, iso)
 MCMC_LAYOUT_UNIT_DECL(lpc, normal)
 MCMC_LAYOUT_UNIT_DECL(lpc, absnormal)

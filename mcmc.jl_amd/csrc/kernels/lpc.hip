@@ -36,4 +36,16 @@ hipError_t mcmc_launch_lpc_eval(const mcmc::KernelArgs& a, const double* xin, do
     }
 }
 
+hipError_t mcmc_launch_lpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st) {
+    using namespace mcmc;
+    if (a.s.d < 1 || a.s.d > 32) return hipErrorInvalidValue;
+    switch (a.m.kind) {
+        case MK_ISO: return mcmc_lpc_record_iso(a, r, st);
+        case MK_NORMAL: return mcmc_lpc_record_normal(a, r, st);
+        case MK_ABS_NORMAL: return mcmc_lpc_record_absnormal(a, r, st);
+        case MK_DIST: return mcmc_lpc_record_dist(a, r, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 int mcmc_lpc_max_d() { return 32; }

@@ -76,6 +76,27 @@ static hipError_t lpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
     return hipGetLastError();
 }
 
+// storeLeaps records (samplers.hpp hmc_record_body), generic mapping only: a diagnostic
+template <int NB, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void lpc_hmc_rec(KernelArgs a, LeapRec r) { hmc_record_body<LaneChain<NB>, M, DA>(a, r); }
+
+template <class M>
+static hipError_t lpc_record_m(const KernelArgs& a, const LeapRec& r, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    const bool da = a.sa.kind == SK_HMCDA;
+#define LPC_REC(NB)                                                       \
+    case NB:                                                              \
+        if (da) lpc_hmc_rec<NB, M, true><<<grid, kBlock, 0, st>>>(a, r);   \
+        else lpc_hmc_rec<NB, M, false><<<grid, kBlock, 0, st>>>(a, r);     \
+        break;
+    switch ((a.s.d + 3) / 4) {
+        LPC_REC(1) LPC_REC(2) LPC_REC(3) LPC_REC(4) LPC_REC(5) LPC_REC(6) LPC_REC(7) LPC_REC(8)
+        default: return hipErrorInvalidValue;
+    }
+#undef LPC_REC
+    return hipGetLastError();
+}
+
 }  // namespace mcmc
 
 // one translation unit per model: LPC_UNIT(iso, IsoDot, true) defines mcmc_lpc_step_iso / mcmc_lpc_eval_iso
@@ -86,6 +107,9 @@ static hipError_t lpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
     hipError_t mcmc_lpc_eval_##name(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, \
                                     int check, hipStream_t st) {                                         \
         return mcmc::lpc_eval_m<mcmc::Model>(a, xin, lp, g, check, st);                                 \
+    }                                                                                                    \
+    hipError_t mcmc_lpc_record_##name(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st) { \
+        return mcmc::lpc_record_m<mcmc::Model>(a, r, st);                                               \
     }
 
 // RAM kernels live in their own translation units (lpc_ram_*.hip, built without machine LICM: hoisted

@@ -27,4 +27,16 @@ hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, do
     }
 }
 
+hipError_t mcmc_launch_wpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st) {
+    using namespace mcmc;
+    if (a.s.d < 1 || a.s.d > 2048) return hipErrorInvalidValue;
+    switch (a.m.kind) {
+        case MK_ISO: return mcmc_wpc_record_iso(a, r, st);
+        case MK_NORMAL: return mcmc_wpc_record_normal(a, r, st);
+        case MK_ABS_NORMAL: return mcmc_wpc_record_absnormal(a, r, st);
+        case MK_DIST: return mcmc_wpc_record_dist(a, r, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 int mcmc_wpc_max_d() { return 2048; }

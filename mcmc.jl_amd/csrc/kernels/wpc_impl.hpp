@@ -76,6 +76,27 @@ static hipError_t wpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
     return hipGetLastError();
 }
 
+// storeLeaps records (samplers.hpp hmc_record_body), generic mapping only: a diagnostic
+template <int NB, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void wpc_hmc_rec(KernelArgs a, LeapRec r) { hmc_record_body<WaveChain<NB>, M, DA>(a, r); }
+
+template <class M>
+static hipError_t wpc_record_m(const KernelArgs& a, const LeapRec& r, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    const bool da = a.sa.kind == SK_HMCDA;
+#define WPC_REC(NB)                                                       \
+    case NB:                                                              \
+        if (da) wpc_hmc_rec<NB, M, true><<<grid, kBlock, 0, st>>>(a, r);   \
+        else wpc_hmc_rec<NB, M, false><<<grid, kBlock, 0, st>>>(a, r);     \
+        break;
+    switch (wpc_nb_for(a.s.d)) {
+        WPC_REC(1) WPC_REC(2) WPC_REC(4) WPC_REC(8)
+        default: return hipErrorInvalidValue;
+    }
+#undef WPC_REC
+    return hipGetLastError();
+}
+
 }  // namespace mcmc
 
 #define WPC_UNIT(name, Model, SPEC)                                                                      \
@@ -85,4 +106,7 @@ static hipError_t wpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
     hipError_t mcmc_wpc_eval_##name(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, \
                                     int check, hipStream_t st) {                                         \
         return mcmc::wpc_eval_m<mcmc::Model>(a, xin, lp, g, check, st);                                 \
+    }                                                                                                    \
+    hipError_t mcmc_wpc_record_##name(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st) { \
+        return mcmc::wpc_record_m<mcmc::Model>(a, r, st);                                               \
     }

@@ -108,6 +108,10 @@ struct LaneChain {
             asm volatile("" : "+v"(o));
         }
     }
+    // storeLeaps records, coordinate-major [l][d][C]: the kept-sample layout
+    __device__ __forceinline__ void store_cm(const StepArgs& s, int64_t l, const double (&v)[NC], double* base) const {
+        store_kept(s, l, v, base);
+    }
     // add this chain's evaluation count to the launch-wide counter (one atomic per wave)
     __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
         if (s.n_evals == nullptr) return;
@@ -212,6 +216,14 @@ struct WaveChain {
     }
     __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
         if (s.n_evals != nullptr && live && lane == 0) atomicAdd(s.n_evals, (unsigned long long)n);
+    }
+    // storeLeaps records, coordinate-major [l][d][C] (scattered 8-byte stores: a diagnostic, not a hot path)
+    __device__ __forceinline__ void store_cm(const StepArgs& s, int64_t l, const double (&v)[NC], double* base) const {
+        if (base == nullptr || !live) return;
+        double* p = base + (size_t)l * (size_t)d * (size_t)s.C + (size_t)c;
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (valid(k)) p[(size_t)coord(k) * (size_t)s.C] = v[k];
     }
     __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
         if (live && lane == 0 && acc && s.acc_bits != nullptr)
@@ -527,6 +539,67 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
         p.store_t(a.st.t_acc, n_acc);
         p.store_t(a.st.t_prop, n_prop);
     }
+}
+
+// ------------------------------------------------------------------ HMC storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117)
+// Records the trajectory the next step (s.step_begin) takes, without moving the chain: leap 0 is state0 after
+// update! (pars, grad, momentum, logTarget, H), leap l the state after the l-th leapfrog (HMC.jl:93-102), for
+// l <= min(nLeaps, cap); nl gets nLeaps.  hmc_body's and trajectory's operations, so the states are bitwise
+// the ones the step computes; the log-target is evaluated after every leapfrog here (the step skips that for
+// function models, where it does not feed back into the trajectory).
+template <class P, class M, bool DA>
+__device__ __forceinline__ void hmc_record_body(const KernelArgs& a, const LeapRec& r) {
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const P p(s);
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const bool tuned = !DA && sa.tuner;
+    const int64_t i = s.step_begin;
+    double x[P::NC], m[P::NC], g[P::NC];
+    p.load(a.st.x, s.ld, x);
+    const double lp = p.load_scalar(a.st.lp);
+    const double eps = (DA || tuned) ? p.load_scalar(a.st.t_step) : sa.leap_step;
+    int64_t nl;
+    if (DA) {
+        const double rr = round_away(sa.len / eps);                  // HMCDA.jl:104
+        nl = rr < 1.0 ? 1 : (rr > (double)sa.max_leaps ? sa.max_leaps : (int64_t)rr);
+    } else {
+        nl = tuned ? (int64_t)p.load_t(a.st.t_leaps) : sa.n_leaps;
+    }
+    gen_normals(p, rs, chain, (uint32_t)i, m);                       // state0.m = randn(model.size)
+    double H = -lp + half_dot(p, m);                                 // update!(state0)
+#pragma unroll
+    for (int k = 0; k < P::NC; ++k) g[k] = model.grad(x[k]);         // the state's gradient (in support)
+    const size_t C = (size_t)s.C;
+    p.store_cm(s, 0, x, r.pars);                                     // leapStates[1] = deepcopy(state0)
+    p.store_cm(s, 0, g, r.grads);
+    p.store_cm(s, 0, m, r.mom);
+    p.store_t(r.lp, lp);
+    p.store_t(r.H, H);
+    bool oos = false;
+    const int64_t nrec = nl < r.cap ? nl : r.cap;
+    for (int64_t l = 1; l <= nrec; ++l) {
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            m[k] = m[k] + (0.5 * g[k]) * eps;                         // n.m += 0.5*n.grad*ve
+            x[k] = x[k] + eps * m[k];                                 // n.pars += ve * n.m
+        }
+        const double lpl = eval_lp(p, model, x, oos);                // calc!(n, ll)
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            g[k] = oos ? 0.0 : model.grad(x[k]);
+            m[k] = m[k] + (0.5 * g[k]) * eps;                         // n.m += 0.5*n.grad*ve
+        }
+        H = -lpl + half_dot(p, m);                                    // update!(n)
+        p.store_cm(s, l, x, r.pars);                                  // leapStates[l+1]
+        p.store_cm(s, l, g, r.grads);
+        p.store_cm(s, l, m, r.mom);
+        p.store_t(r.lp + (size_t)l * C, lpl);
+        p.store_t(r.H + (size_t)l * C, H);
+    }
+    p.store_t(r.nl, (int32_t)nl);
 }
 
 // ------------------------------------------------------------------ RAM

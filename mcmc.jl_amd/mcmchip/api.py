@@ -330,9 +330,12 @@ class HMC(_Sampler):
             raise AssertionError("inner steps should be > 0")                  # HMC.jl:60
         if not e > 0:
             raise AssertionError("inner steps scaling should be > 0")          # HMC.jl:61
-        if storeLeaps:
-            raise NotImplementedError("storeLeaps diagnostics are not produced by the batched kernels")
         self.nLeaps, self.leapStep, self.tuner = n, e, tuner
+        self.storeLeaps = bool(storeLeaps)
+
+    def leaps_cap(self) -> int:
+        """leapfrog states stored per kept step (storeLeaps): nLeaps, or the tuner's maxStep bound"""
+        return max(self.nLeaps, self.tuner.maxStep) if self.tuner is not None else self.nLeaps
 
     def cfg(self):
         c = super().cfg()
@@ -354,10 +357,14 @@ class HMCDA(_Sampler):
             raise AssertionError(f"shrinkage parameter of HMCDA sampler ({shrinkage}) must be positive")
         if not t0 >= 0:
             raise AssertionError(f"t0 parameter of HMCDA sampler ({t0}) must be non-negative")
-        if storeLeaps:
-            raise NotImplementedError("storeLeaps diagnostics are not produced by the batched kernels")
         self.rate, self.len, self.shrinkage, self.t0, self.step = rate, len, shrinkage, t0, step
         self.max_leaps = int(max_leaps)
+        self.storeLeaps = bool(storeLeaps)
+
+    def leaps_cap(self) -> int:
+        """leapfrog states stored per kept step (storeLeaps): max_leaps when set, else 256 (the trajectory
+        length round(len / leapStep) adapts; diagnostics["leaps"]["nleaps"] always holds the full count)"""
+        return self.max_leaps if self.max_leaps > 0 else 256
 
     def cfg(self):
         c = super().cfg()
@@ -590,9 +597,21 @@ def _run_task(t: MCMCTask) -> MCMCChain:
     out.final_x = fx.ctypes.data
     out.final_lp = flp.ctypes.data
     out.on_device = 0
+    leaps = None
+    if getattr(t.sampler, "storeLeaps", False):              # HMC.jl:145-150 / HMCDA.jl:110-117
+        cap = t.sampler.leaps_cap()
+        leaps = {"pars": np.empty((nk, cap + 1, d, C)), "grad": np.empty((nk, cap + 1, d, C)),
+                 "m": np.empty((nk, cap + 1, d, C)), "logTarget": np.empty((nk, cap + 1, C)),
+                 "H": np.empty((nk, cap + 1, C)), "nleaps": np.empty((nk, C), dtype=np.int32)}
+        check(lib.mcmc_chains_store_leaps(h, cap, *(leaps[k].ctypes.data for k in
+                                                    ("pars", "grad", "m", "logTarget", "H", "nleaps"))))
     cfg = r.cfg()
     check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
     diags = {"step": list(r.r), "accept": _unpack_bits(bits, C)}
+    if leaps is not None:
+        # per kept step: the trajectory's states, leap 0 = state0 (the reference's leapStates array of
+        # HMCSample(pars, grad, m, logTarget, H)), NaN past nleaps
+        diags["leaps"] = leaps
     return MCMCChain(r.r, samples, grads, diags, t, out.runtime_s, out.kernel_ms, fx, flp)
 
 

@@ -463,11 +463,32 @@ static void orc_ram_update(double* Lc, int64_t C, int d, int64_t i, double ratio
     }
 }
 
+/* storeLeaps record (HMC.jl:145-150): pars / grads / mom [nkept][cap+1][d][C], lp / H [nkept][cap+1][C],
+   nl [nkept][C] */
+typedef struct {
+    int64_t cap;
+    double *pars, *grads, *mom, *lp, *H;
+    int32_t* nl;
+} orc_leaps;
+
+static void orc_leap_put(const orc_leaps* lv, int64_t kk, int64_t l, int d, int64_t C, int64_t c, const double* x,
+                         const double* g, const double* mom, double lp, double H) {
+    const size_t base = (size_t)kk * (size_t)(lv->cap + 1) + (size_t)l;
+    for (int j = 0; j < d; ++j) {
+        lv->pars[(base * d + j) * C + c] = x[j];
+        lv->grads[(base * d + j) * C + c] = g[j];
+        lv->mom[(base * d + j) * C + c] = mom[j];
+    }
+    lv->lp[base * C + c] = lp;
+    lv->H[base * C + c] = H;
+}
+
 /* ------------------------------------------------------------ one chain */
 /* `len` steps of SerialMC (SerialMC.jl:47-67) for chain c, sampler loop counter continuing from step0. */
 static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, uint32_t chain, int64_t c,
                       int64_t C, int64_t step0, int64_t burnin, int64_t thinning, int64_t len, orc_state* st,
-                      double* samples, double* grads, uint8_t* acc_out, int order, double* buf) {
+                      double* samples, double* grads, uint8_t* acc_out, int order, double* buf,
+                      const orc_leaps* lv) {
     const int d = m->d;
     double* x = buf;          /* state: pars */
     double* g = x + d;        /* state: grad */
@@ -575,7 +596,20 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 nl = nl_fixed;
             }
             n_evals += nl;
-            double lpl = orc_trajectory(m, eps, nl, xp, mom, gp, lp, tmp, order);
+            int64_t kk_rec = 0;
+            double lpl;
+            if (lv && orc_kept(i - step0, burnin, thinning, len, &kk_rec)) {
+                /* storeLeaps: leapStates[1] = state0, then the state after every leapfrog (HMC.jl:145-150) */
+                orc_leap_put(lv, kk_rec, 0, d, C, c, xp, gp, mom, lp, H0);
+                lpl = lp;
+                for (int64_t l = 1; l <= nl; ++l) {
+                    lpl = orc_trajectory(m, eps, 1, xp, mom, gp, lpl, tmp, order);
+                    if (l <= lv->cap) orc_leap_put(lv, kk_rec, l, d, C, c, xp, gp, mom, lpl, -lpl + 0.5 * orc_dot(mom, m, order));
+                }
+                lv->nl[(size_t)kk_rec * C + c] = (int32_t)nl;
+            } else {
+                lpl = orc_trajectory(m, eps, nl, xp, mom, gp, lp, tmp, order);
+            }
             const double H = -lpl + 0.5 * orc_dot(mom, m, order);
             const double u = orc_accept_uniform(seed, chain, (uint32_t)i);
             if (da) {
@@ -680,9 +714,10 @@ int64_t orc_init(const orc_model* m, const orc_sampler* s, int64_t C, orc_state*
 
 /* run_serialmc over chains [c_begin, c_end) of a batch of C (SerialMC.jl:37-85).
    samples/grads: [nkept][d][C]; acc_out: [nkept][C] bytes.  nthreads > 1 uses OpenMP. */
-void orc_run(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t chain0, int64_t C,
-             int64_t c_begin, int64_t c_end, int64_t step0, int64_t burnin, int64_t thinning, int64_t len,
-             orc_state* st, double* samples, double* grads, uint8_t* acc_out, int order, int nthreads) {
+static void orc_run_impl(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t chain0, int64_t C,
+                         int64_t c_begin, int64_t c_end, int64_t step0, int64_t burnin, int64_t thinning, int64_t len,
+                         orc_state* st, double* samples, double* grads, uint8_t* acc_out, int order, int nthreads,
+                         const orc_leaps* lv) {
     const int d = m->d;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
@@ -694,10 +729,27 @@ void orc_run(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t ch
 #endif
         for (int64_t c = c_begin; c < c_end; ++c)
             orc_chain(m, s, seed, (uint32_t)(chain0 + c), c, C, step0, burnin, thinning, len, st, samples, grads,
-                      acc_out, order, buf);
+                      acc_out, order, buf, lv);
         free(buf);
     }
     (void)nthreads;
+}
+
+void orc_run(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t chain0, int64_t C,
+             int64_t c_begin, int64_t c_end, int64_t step0, int64_t burnin, int64_t thinning, int64_t len,
+             orc_state* st, double* samples, double* grads, uint8_t* acc_out, int order, int nthreads) {
+    orc_run_impl(m, s, seed, chain0, C, c_begin, c_end, step0, burnin, thinning, len, st, samples, grads, acc_out,
+                 order, nthreads, NULL);
+}
+
+/* orc_run with the storeLeaps record of every kept HMC / HMCDA step (buffers as mcmc_chains_store_leaps) */
+void orc_run_leaps(const orc_model* m, const orc_sampler* s, uint64_t seed, int64_t chain0, int64_t C,
+                   int64_t step0, int64_t burnin, int64_t thinning, int64_t len, orc_state* st, double* samples,
+                   double* grads, uint8_t* acc_out, int order, int64_t cap, double* lpars, double* lgrads,
+                   double* lmom, double* llp, double* lH, int32_t* lnl) {
+    orc_leaps lv = {cap, lpars, lgrads, lmom, llp, lH, lnl};
+    orc_run_impl(m, s, seed, chain0, C, 0, C, step0, burnin, thinning, len, st, samples, grads, acc_out, order, 1,
+                 &lv);
 }
 
 /* model.eval / evalallg on a batch x[d][C] */

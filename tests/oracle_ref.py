@@ -147,6 +147,28 @@ class OracleChains:
             raise AssertionError("Initial values out of model support, try other values")
         self.steps_done = 0
 
+    def run_leaps(self, runner, cap):
+        """run() with the storeLeaps record (mcmc_chains_store_leaps layout); returns (samples, grads, accept,
+        leaps dict with pars / grad / m [nkept][cap+1][d][C], logTarget / H [nkept][cap+1][C], nleaps [nkept][C])"""
+        d, C = self.om.size, self.C
+        nk = len(runner.r)
+        samples = np.full((nk, d, C), np.nan)
+        grads = np.full((nk, d, C), np.nan)
+        acc = np.zeros((nk, C), dtype=np.uint8)
+        lv = {"pars": np.full((nk, cap + 1, d, C), np.nan), "grad": np.full((nk, cap + 1, d, C), np.nan),
+              "m": np.full((nk, cap + 1, d, C), np.nan), "logTarget": np.full((nk, cap + 1, C), np.nan),
+              "H": np.full((nk, cap + 1, C), np.nan), "nleaps": np.zeros((nk, C), dtype=np.int32)}
+        L = lib()
+        L.orc_run_leaps.restype = None
+        L.orc_run_leaps(ct.byref(self.om.s), ct.byref(self.os), ct.c_uint64(self.seed), ct.c_int64(self.chain0),
+                        ct.c_int64(C), ct.c_int64(self.steps_done), ct.c_int64(runner.burnin),
+                        ct.c_int64(runner.thinning), ct.c_int64(runner.len), ct.byref(self.st), _d(samples), _d(grads),
+                        acc.ctypes.data_as(ct.POINTER(ct.c_uint8)), ct.c_int(self.order), ct.c_int64(cap),
+                        _d(lv["pars"]), _d(lv["grad"]), _d(lv["m"]), _d(lv["logTarget"]), _d(lv["H"]),
+                        lv["nleaps"].ctypes.data_as(ct.POINTER(ct.c_int32)))
+        self.steps_done += runner.len
+        return samples, grads, acc, lv
+
     def run(self, runner, nthreads=None, c_begin=0, c_end=None, want_grads=True):
         d, C = self.om.size, self.C
         nk = len(runner.r)

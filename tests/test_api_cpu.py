@@ -163,3 +163,13 @@ def test_accept_bit_unpacking():
             if acc[k, c]:
                 words[k, c // 64] |= np.uint64(1) << np.uint64(c % 64)
     assert np.array_equal(_unpack_bits(words, C), acc.T)
+
+
+def test_store_leaps_options():
+    """storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117) is accepted; the record keeps nLeaps (or the tuner's maxStep,
+    or HMCDA's max_leaps) states per kept step"""
+    assert mc.HMC(4, 0.3, storeLeaps=True).leaps_cap() == 4
+    assert mc.HMC(3, 0.9, mc.EmpMCTuner(0.7, maxStep=9), storeLeaps=True).leaps_cap() == 9
+    assert mc.HMCDA(storeLeaps=True, max_leaps=40).leaps_cap() == 40
+    assert mc.HMCDA(storeLeaps=True).leaps_cap() == 256
+    assert not mc.HMC().storeLeaps

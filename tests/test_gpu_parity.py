@@ -483,3 +483,38 @@ def test_ram_limits(gpu):
     m = _glm_model("linear", 40)
     with pytest.raises(mc.MCMCError, match="RAM is built for d <= 32"):
         mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
+
+
+# ------------------------------------------------------------------ storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117)
+def _store_leaps_case(m, sp, C, seed, order, cap, steps=16, burnin=5, thinning=3):
+    r = mc.SerialMC(steps=steps, burnin=burnin, thinning=thinning)
+    chain = mc.run((m * sp * r).batch(C, seed=seed))
+    lv = chain.diagnostics["leaps"]
+    oc = orc.OracleChains(m, sp, nchains=C, seed=seed, order=order)
+    s_ref, g_ref, acc_ref, lv_ref = oc.run_leaps(r, cap)
+    assert np.array_equal(chain._samples.view(np.uint64), s_ref.view(np.uint64))   # the run itself is unchanged
+    assert np.array_equal(chain.diagnostics["accept"].T, acc_ref.astype(bool))
+    assert np.array_equal(lv["nleaps"], lv_ref["nleaps"])
+    for k in ("pars", "grad", "m", "logTarget", "H"):
+        a, b = lv[k], lv_ref[k]
+        assert a.shape == b.shape
+        assert np.array_equal(np.isnan(a), np.isnan(b)), k                         # NaN past nLeaps
+        assert np.array_equal(np.nan_to_num(a).view(np.uint64), np.nan_to_num(b).view(np.uint64)), k
+
+
+@pytest.mark.parametrize("sname", ["hmc", "hmc_tuned", "hmcda"])
+@pytest.mark.parametrize("mkind,d", [("iso", 3), ("normal", 16), ("iso", 40), ("abs", 300)])
+def test_store_leaps_bitwise(gpu, sname, mkind, d):
+    """the trajectory record of every kept step, lane-per-chain (d <= 32) and wave-per-chain kernels"""
+    sp = {"hmc": lambda: mc.HMC(4, 0.3, storeLeaps=True),
+          "hmc_tuned": lambda: mc.HMC(3, 0.9, mc.EmpMCTuner(0.7, adaptStep=5, maxStep=9), storeLeaps=True),
+          "hmcda": lambda: mc.HMCDA(len=0.8, storeLeaps=True, max_leaps=40)}[sname]()
+    _store_leaps_case(_model(mkind, d), sp, C=70, seed=31 + d, order=order_for(d), cap=sp.leaps_cap())
+
+
+@pytest.mark.parametrize("sname", ["hmc", "hmcda"])
+@pytest.mark.parametrize("kind,d", [("logistic", 5), ("linear", 37), ("linear", 200)])
+def test_store_leaps_regression_bitwise(gpu, sname, kind, d):
+    """the trajectory record on the fp64-MFMA regression kernels (single-slice and d-sliced)"""
+    sp = mc.HMC(3, 0.02, storeLeaps=True) if sname == "hmc" else mc.HMCDA(len=0.1, storeLeaps=True, max_leaps=30)
+    _store_leaps_case(_glm_model(kind, d), sp, C=40, seed=5 + d, order=0, cap=sp.leaps_cap())

@@ -173,8 +173,8 @@ def leapfrog(s, ve, model):
     return n
 
 
-def hmc_task(model, s, burnin, seed, chain):
-    """HMC.jl:106-175 (EmpiricalHMCTune / adapt!: HMC.jl:20-47)"""
+def hmc_task(model, s, burnin, seed, chain, rec=None):
+    """HMC.jl:106-175 (EmpiricalHMCTune / adapt!: HMC.jl:20-47); rec: storeLeaps, every step's leapStates"""
     state0 = HMCSample(model.init.copy())
     state0.calc(model)
     tune = ({"nLeaps": s.nLeaps, "leapStep": s.leapStep, "accepted": 0, "proposed": 0}
@@ -189,8 +189,12 @@ def hmc_task(model, s, burnin, seed, chain):
         state0.m = randn(seed, chain, int(i), len(state0.pars))
         state0.update()
         state = state0.copy()
+        leapStates = [state0.copy()]                                # HMC.jl:145-150 (storeLeaps)
         for _ in range(int(nLeaps)):
             state = leapfrog(state, leapStep, model)
+            leapStates.append(state.copy())
+        if rec is not None:
+            rec.append(leapStates)
         if rand(seed, chain, int(i)) < jexp(state0.H - state.H):
             yield state.pars, state.grad, True
             state0 = state.copy()
@@ -217,8 +221,8 @@ def jmin(a, b):
     return float(np.fmin(a, b))
 
 
-def hmcda_task(model, s, burnin, seed, chain):
-    """HMCDA.jl:72-143 with initializeHMCDAStep (:51-69)"""
+def hmcda_task(model, s, burnin, seed, chain, rec=None):
+    """HMCDA.jl:72-143 with initializeHMCDAStep (:51-69); rec: storeLeaps, every step's leapStates"""
     state0 = HMCSample(model.init.copy())
     state0.calc(model)
     # state0.m = randn(model.size); leapStep = initializeHMCDAStep(model, state0): state0.H is still NaN
@@ -237,8 +241,12 @@ def hmcda_task(model, s, burnin, seed, chain):
         state0.update()
         state = state0.copy()
         nLeaps = max(1, julia02_round(s.len / leapStep))
+        leapStates = [state0.copy()]                                # HMCDA.jl:110-117 (storeLeaps)
         for _ in range(int(nLeaps)):
             state = leapfrog(state, leapStep, model)
+            leapStates.append(state.copy())
+        if rec is not None:
+            rec.append(leapStates)
         p = jmin(1.0, jexp(state0.H - state.H))
         if rand(seed, chain, int(i)) < p:
             yield state.pars, state.grad, True
@@ -397,3 +405,33 @@ def test_oracle_matches_literal_regression_examples(sname, kind):
         np.testing.assert_allclose(s_orc[:, :, c], np.array(kept), rtol=RTOL, atol=1e-12)
         if g_orc is not None and grads[0] is not None:
             np.testing.assert_allclose(g_orc[:, :, c], np.array(grads), rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("sname", ["hmc", "hmc_tuned", "hmcda"])
+@pytest.mark.parametrize("kind", ["iso", "normal"])
+def test_oracle_store_leaps_matches_literal_reference(sname, kind):
+    """storeLeaps: the oracle's record of every kept step's trajectory against the literal leapStates"""
+    d, steps, burnin, thinning, C, seed, cap = 5, 20, 8, 3, 6, 99, 12
+    m, lit = _models(kind, d)
+    sp = SAMPLERS[sname]()
+    oc = orc.OracleChains(m, sp, nchains=C, seed=seed)
+    runner = mc.SerialMC(steps=steps, burnin=burnin, thinning=thinning)
+    s_orc, _, a_orc, lv = oc.run_leaps(runner, cap)
+    s_ref, _, a_ref = orc.OracleChains(m, sp, nchains=C, seed=seed).run(runner, nthreads=1)
+    assert np.array_equal(s_orc.view(np.uint64), s_ref.view(np.uint64))      # recording does not perturb the run
+    assert np.array_equal(a_orc, a_ref)
+    kept = list(range(burnin + 1, steps + 1, thinning))
+    for c in range(C):
+        rec = []
+        run_serialmc(TASKS[sp.kind](lit, sp, burnin, seed, c, rec=rec), steps, burnin, thinning)
+        for kk, i in enumerate(kept):
+            states = rec[i - 1]
+            nl = len(states) - 1
+            assert lv["nleaps"][kk, c] == nl
+            for l, st in enumerate(states[:cap + 1]):
+                np.testing.assert_allclose(lv["pars"][kk, l, :, c], st.pars, rtol=RTOL, atol=1e-12)
+                np.testing.assert_allclose(lv["grad"][kk, l, :, c], st.grad, rtol=RTOL, atol=1e-12)
+                np.testing.assert_allclose(lv["m"][kk, l, :, c], st.m, rtol=RTOL, atol=1e-12)
+                np.testing.assert_allclose(lv["logTarget"][kk, l, c], st.logTarget, rtol=RTOL, atol=1e-12)
+                np.testing.assert_allclose(lv["H"][kk, l, c], st.H, rtol=RTOL, atol=1e-12)
+            assert np.isnan(lv["H"][kk, min(nl, cap) + 1:, c]).all()
