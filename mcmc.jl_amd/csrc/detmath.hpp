@@ -355,7 +355,9 @@ __device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, dou
                                                   const double (*sct)[2] = kBmSinCosTab) {
     const uint32_t t = w + 0x800000u;
     const uint32_t k = t >> 24;
-    const double r = (double)((int32_t)(t & 0xffffffu) - 0x800000) * 0x1.921fb54442d18p-30;
+    // j = (t & 0xffffff) - 2^23 is the sign-extended low 24 bits of w (checked for all 2^32 w): one v_bfe_i32.
+    // (Written as shifts: __builtin_amdgcn_sbfe here was followed by an unsigned int-to-double conversion.)
+    const double r = (double)(((int32_t)(w << 8)) >> 8) * 0x1.921fb54442d18p-30;
     const double r2 = r * r;
     double sp = __builtin_fma(r2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);   // -1/5040, 1/120
     sp = __builtin_fma(r2, sp, -0x1.5555555555555p-3);                             // -1/6
