@@ -93,31 +93,31 @@ class NormalDSL:
 
 
 # ------------------------------------------------------------------ samplers (yield MCMCSample.ppars, pgrads, accept)
-def rwm_task(model, s, burnin, seed, chain):
+def rwm_task(model, s, burnin, seed, chain, step0=0):
     """RWM.jl:43-72"""
     scale = model.scale * s.scale                                   # model.scale .* sampler.scale
     pars = model.init.copy()
     logTarget = model.eval(pars)
     assert math.isfinite(logTarget)
-    i = 0
+    i = step0
     while True:
         i += 1
         proposedPars = pars + randn(seed, chain, i, len(pars)) * scale
         proposedLogTarget = model.eval(proposedPars)
         ratio = proposedLogTarget - logTarget
         if ratio > 0 or (ratio > math.log(rand(seed, chain, i))):
-            yield proposedPars, None, True
+            yield proposedPars, None, True, proposedLogTarget
             pars, logTarget = proposedPars.copy(), proposedLogTarget
         else:
-            yield pars, None, False
+            yield pars, None, False, logTarget
 
 
-def mala_task(model, s, burnin, seed, chain):
+def mala_task(model, s, burnin, seed, chain, step0=0):
     """MALA.jl:65-126 (EmpiricalMALATune / adapt!: MALA.jl:19-43)"""
     pars = model.init.copy()
     logTarget, grad = model.evalallg(pars)
     tune = {"driftStep": s.driftStep, "accepted": 0, "proposed": 0} if s.tuner is not None else None
-    i = 1
+    i = step0 + 1
     while True:
         if tune is not None:
             tune["proposed"] += 1
@@ -132,12 +132,12 @@ def mala_task(model, s, burnin, seed, chain):
         probOldGivenNew = np.sum(-(parsMean - pars) ** 2 / (2 * driftStep) - math.log(2 * math.pi * driftStep) / 2)
         ratio = proposedLogTarget + probOldGivenNew - logTarget - probNewGivenOld
         if ratio > 0 or (ratio > math.log(rand(seed, chain, i))):
-            yield proposedPars, proposedGrad, True
+            yield proposedPars, proposedGrad, True, proposedLogTarget
             pars, logTarget, grad = proposedPars.copy(), proposedLogTarget, proposedGrad.copy()
             if tune is not None:
                 tune["accepted"] += 1
         else:
-            yield pars, grad, False
+            yield pars, grad, False, logTarget
         if tune is not None and i <= burnin and i % s.tuner.adaptStep == 0:
             rate = tune["accepted"] / tune["proposed"]
             tune["driftStep"] *= (1 / (1 + jexp(-11 * (rate - s.tuner.targetRate))) + 0.5)
@@ -173,13 +173,13 @@ def leapfrog(s, ve, model):
     return n
 
 
-def hmc_task(model, s, burnin, seed, chain, rec=None):
+def hmc_task(model, s, burnin, seed, chain, rec=None, step0=0):
     """HMC.jl:106-175 (EmpiricalHMCTune / adapt!: HMC.jl:20-47); rec: storeLeaps, every step's leapStates"""
     state0 = HMCSample(model.init.copy())
     state0.calc(model)
     tune = ({"nLeaps": s.nLeaps, "leapStep": s.leapStep, "accepted": 0, "proposed": 0}
             if s.tuner is not None else None)
-    i = 1.0                                                          # for i in 1:Inf
+    i = float(step0 + 1)                                             # for i in 1:Inf
     while True:
         if tune is not None:
             tune["proposed"] += 1
@@ -196,12 +196,12 @@ def hmc_task(model, s, burnin, seed, chain, rec=None):
         if rec is not None:
             rec.append(leapStates)
         if rand(seed, chain, int(i)) < jexp(state0.H - state.H):
-            yield state.pars, state.grad, True
+            yield state.pars, state.grad, True, state.logTarget
             state0 = state.copy()
             if tune is not None:
                 tune["accepted"] += 1
         else:
-            yield state0.pars, state0.grad, False
+            yield state0.pars, state0.grad, False, state0.logTarget
         if tune is not None and i <= burnin and i % s.tuner.adaptStep == 0:
             t = tune
             t["rate"] = t["accepted"] / t["proposed"]
@@ -249,10 +249,10 @@ def hmcda_task(model, s, burnin, seed, chain, rec=None):
             rec.append(leapStates)
         p = jmin(1.0, jexp(state0.H - state.H))
         if rand(seed, chain, int(i)) < p:
-            yield state.pars, state.grad, True
+            yield state.pars, state.grad, True, state.logTarget
             state0 = state.copy()
         else:
-            yield state0.pars, state0.grad, False
+            yield state0.pars, state0.grad, False, state0.logTarget
         if i < burnin:
             eta = 1 / (i + s.t0)
             dualH = (1 - eta) * dualH + eta * (s.rate - p)
@@ -272,7 +272,7 @@ def run_serialmc(task, steps, burnin, thinning):
     r = range(burnin + 1, steps + 1, thinning)
     kept, grads, acc = [], [], []
     for i in range(1, steps + 1):
-        ppars, pgrads, accept = next(task)
+        ppars, pgrads, accept, _ = next(task)
         if i in r:
             kept.append(np.array(ppars, float))
             grads.append(None if pgrads is None else np.array(pgrads, float))
@@ -435,3 +435,100 @@ def test_oracle_store_leaps_matches_literal_reference(sname, kind):
                 np.testing.assert_allclose(lv["logTarget"][kk, l, c], st.logTarget, rtol=RTOL, atol=1e-12)
                 np.testing.assert_allclose(lv["H"][kk, l, c], st.H, rtol=RTOL, atol=1e-12)
             assert np.isnan(lv["H"][kk, min(nl, cap) + 1:, c]).all()
+
+
+
+# ------------------------------------------------------------------ SeqMC (SeqMC.jl:39-122)
+class AbsNormalDSL:
+    """y = abs(x); y ~ Normal(mu, sigma)  (README.md SeqMC example), LLAcc sum"""
+
+    def __init__(self, mu, sigma, init):
+        self.mu, self.sigma = mu, sigma
+        self.init = np.asarray(init, float)
+        self.scale = np.ones(len(self.init))
+
+    def eval(self, v):
+        acc = 0.0
+        for x in v:
+            z = (abs(x) - self.mu) / self.sigma
+            acc += -0.5 * (z * z + math.log(2 * math.pi)) - math.log(self.sigma)
+            if not math.isfinite(acc):
+                return -math.inf
+        return acc
+
+
+class _Reset:
+    """MCMC.reset(t, pars): the task continues from pars (task_local_storage(:reset), RWM.jl:49)"""
+
+    def __init__(self, model, pars):
+        self.m, self.init, self.scale = model, np.array(pars, float), model.scale
+
+    def eval(self, v):
+        return self.m.eval(v)
+
+    def evalallg(self, v):
+        return self.m.evalallg(v)
+
+
+def literal_seqmc(targets, particles, steps, burnin, trigger, seed):
+    """run_seqmc (SeqMC.jl:39-122) statement by statement.  targets: [(literal model, sampler, task seed)].
+    The task of target t consumed for particle n at outer step i is chain n's sampler step i of that target
+    (the build's batched counter); the resampling draw is rand() from block (n, i, t, RESAMPLE=2)."""
+    npart = len(particles)
+    pars = [np.array(p, float) for p in particles]
+    logW = np.zeros(npart)
+    logtarget = np.zeros(npart)
+    samples, weights, flags = [], [], []
+    for i in range(1, steps + 1):
+        fl = []
+        for t, (lit, sp, ts) in enumerate(targets):
+            for n in range(npart):
+                reset = _Reset(lit, pars[n])                      # MCMC.reset(t, pars[n])
+                ll0 = reset.eval(reset.init)                      # sample.logtarget: the reset state's
+                ppars, _, _, plogtarget = next(TASKS[sp.kind](reset, sp, 0, ts, n, step0=i - 1))
+                pars[n] = np.array(ppars, float)
+                logW[n] += ll0 - logtarget[n]
+                logtarget[n] = plogtarget
+            W = np.exp(logW)
+            fl.append(bool(np.var(W, ddof=1) < trigger))         # Julia var: n - 1 denominator
+            if fl[-1]:
+                cp = np.cumsum(W) / np.sum(W)
+                rs = [0] * npart
+                for n in range(npart):
+                    w = _block(seed, n, i, t, 2)
+                    l = float(((w[0] >> 5) << 26) | (w[1] >> 6)) * 2.0**-53
+                    rs[n] = int(np.argmax(cp >= l))               # findfirst(p -> p >= l, cp)
+                pars = [pars[r].copy() for r in rs]
+                logW = np.zeros(npart)
+                logtarget = logtarget[rs]
+        flags.append(fl)
+        logtarget = np.zeros(npart)
+        if i > burnin:
+            samples.append(np.array(pars).T.copy())
+            weights.append(np.exp(logW))
+    return np.array(samples), np.array(weights), np.array(flags, dtype=np.int32)
+
+
+@pytest.mark.parametrize("trigger", [0.0, 1e9, 0.02])
+def test_oracle_seqmc_matches_literal_reference(trigger):
+    """the oracle's SeqMC (orc_seqmc) against the literal run_seqmc: resampling never, always, data-driven"""
+    npart, steps, burnin, seed = 40, 6, 2, 17
+    sigmas = [3.0, 1.0, 0.5]
+    parts = np.linspace(-2, 2, npart)[:, None] * np.array([[1.0, -0.5]])
+    tg_orc, tg_lit = [], []
+    for k, sg in enumerate(sigmas):
+        m = mc.model(mc.AbsNormalDSL(1.0, sg), x=np.array([0.5, 0.5]), gradient=True)
+        sp = mc.RWM(0.4) if k != 1 else mc.MALA(0.05)
+        tg_orc.append((m, sp))
+        lit = AbsNormalDSL(1.0, sg, [0.5, 0.5])
+        if k == 1:                                                  # MALA needs the gradient: d|x|/dx = sign(x)
+            lit.evalallg = (lambda L: lambda v: (L.eval(v), np.sign(v) * (L.mu - np.abs(v)) / L.sigma**2
+                                                  if math.isfinite(L.eval(v)) else np.zeros(len(v))))(lit)
+        tg_lit.append((lit, sp, 100 + k))
+    s_o, w_o, f_o = orc.seqmc(tg_orc, parts, steps, burnin, trigger, seed, [100, 101, 102])
+    s_l, w_l, f_l = literal_seqmc(tg_lit, parts, steps, burnin, trigger, seed)
+    assert np.array_equal(f_o, f_l)
+    np.testing.assert_allclose(s_o, s_l, rtol=RTOL, atol=1e-12)
+    np.testing.assert_allclose(w_o, w_l, rtol=1e-9, atol=1e-300)
+    if trigger == 0.02:
+        assert 0 < f_o.sum() < f_o.size                              # the data-driven case does both
