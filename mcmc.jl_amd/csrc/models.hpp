@@ -35,6 +35,8 @@ constexpr double kTwoPi = 0x1.921fb54442d18p+2;    // 2*pi rounded (Julia 2*pi)
 
 struct IsoDot {
     static constexpr bool kLLAcc = false;
+    // 0.5 * grad(v) = 0.5 * (-2 v) is -v exactly while |v| < 2^1023 (samplers.hpp trajectory_halfneg)
+    static constexpr bool kHalfGradNeg = true;
     __device__ explicit IsoDot(const ModelArgs&) {}
     __device__ __forceinline__ void acc(double& a, double v) const { a = __builtin_fma(v, v, a); }
     __device__ __forceinline__ double finish(double a) const { return -a; }
@@ -43,6 +45,7 @@ struct IsoDot {
 
 struct NormalDSL {
     static constexpr bool kLLAcc = true;
+    static constexpr bool kHalfGradNeg = false;
     double mu, sigma, logsig, s2;
     __device__ explicit NormalDSL(const ModelArgs& m) : mu(m.mu), sigma(m.sigma) {
         logsig = det_log(sigma);
@@ -58,6 +61,7 @@ struct NormalDSL {
 
 struct AbsNormalDSL {
     static constexpr bool kLLAcc = true;
+    static constexpr bool kHalfGradNeg = false;
     double mu, sigma, logsig, s2;
     __device__ explicit AbsNormalDSL(const ModelArgs& m) : mu(m.mu), sigma(m.sigma) {
         logsig = det_log(sigma);
@@ -83,6 +87,7 @@ struct AbsNormalDSL {
 // the switch is a scalar branch.
 struct DistDSL {
     static constexpr bool kLLAcc = true;
+    static constexpr bool kHalfGradNeg = false;
     int32_t dist;
     double p1, p2, c;
     __device__ explicit DistDSL(const ModelArgs& m) : dist(m.dist), p1(m.mu), p2(m.sigma), c(m.dconst) {

@@ -64,6 +64,7 @@ struct LaneChain {
     __device__ __forceinline__ bool valid(int k) const { return FULL || k < 4 * (NB - 1) || k < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)b; }
     __device__ __forceinline__ double reduce(double v) const { return v; }
+    __device__ __forceinline__ bool any(bool v) const { return v; }
     // running addresses (see store_kept): no per-coordinate uniform offsets live across the step loop
     // (the opaque value is the element offset, not the pointer, so the accesses stay global_*, not flat_*)
     __device__ __forceinline__ void load(const double* x, int64_t ld, double (&v)[NC]) const {
@@ -168,6 +169,7 @@ struct WaveChain {
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + 64 * b); }
     __device__ __forceinline__ double reduce(double v) const { return wave_sum(v); }
+    __device__ __forceinline__ bool any(bool v) const { return __ballot(v) != 0; }
     __device__ __forceinline__ void load(const double* x, int64_t /*ld*/, double (&v)[NC]) const {
         const double* row = x + (size_t)(live ? c : 0) * (size_t)ldr;
 #pragma unroll
@@ -438,6 +440,37 @@ __device__ __forceinline__ double trajectory(const P& p, const M& model, double 
     return lpl;
 }
 
+// The same trajectory for a model whose half gradient 0.5 * (-2 x) is -x (IsoDot): the half kick is (-x) eps, one
+// multiply instead of three, and bitwise trajectory()'s whenever |x| < 2^1023 (then -2x cannot overflow and
+// the halving is exact, subnormals included).  big reports an |x| >= 2^1023 (or non-finite) anywhere on the
+// path, where -2x would have overflowed: the caller then redoes the trajectory with trajectory().
+template <class P, class M>
+__device__ __forceinline__ double trajectory_halfneg(const P& p, const M& model, double eps, int64_t nl,
+                                                     double (&x)[P::NC], double (&m)[P::NC], bool& big) {
+    double kick[P::NC];
+    double xmax = 0.0;
+#pragma unroll
+    for (int k = 0; k < P::NC; ++k) {
+        kick[k] = (-x[k]) * eps;
+        xmax = __builtin_fmax(xmax, __builtin_fabs(x[k]));
+    }
+    for (int64_t l = 0; l < nl; ++l) {
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k) {
+            m[k] = m[k] + kick[k];                                  // n.m += 0.5*n.grad*ve
+            x[k] = x[k] + eps * m[k];                               // n.pars += ve * n.m
+            kick[k] = (-x[k]) * eps;                                // 0.5*n.grad*ve at the new point
+            xmax = __builtin_fmax(xmax, __builtin_fabs(x[k]));
+            m[k] = m[k] + kick[k];                                  // n.m += 0.5*n.grad*ve
+        }
+    }
+    big = p.any(!(xmax < 0x1p1023) && p.live);
+    double lpl = 0.0;
+    bool oos;
+    if (nl > 0) lpl = eval_lp(p, model, x, oos);                    // calc!(n, ll) of the last leapfrog
+    return lpl;
+}
+
 template <class P, class M, bool DA>
 __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
     const StepArgs& s = a.s;
@@ -477,7 +510,19 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             nl = nl_fixed;
         }
         n_evals += nl;
-        const double lpl = trajectory(p, model, eps, nl, x, m);
+        double lpl;
+        if constexpr (M::kHalfGradNeg) {
+            bool big;
+            lpl = trajectory_halfneg(p, model, eps, nl, x, m, big);
+            if (big) {                                          // -2x overflowed somewhere: the exact path
+#pragma unroll
+                for (int k = 0; k < P::NC; ++k) x[k] = x0[k];
+                gen_normals(p, rs, chain, (uint32_t)i, m);
+                lpl = trajectory(p, model, eps, nl, x, m);
+            }
+        } else {
+            lpl = trajectory(p, model, eps, nl, x, m);
+        }
         const double H = -lpl + half_dot(p, m);
         const u32x4 w = rs.block(chain, (uint32_t)i, 0u, TAG_ACCEPT);
         const double u = uniform53(w.x, w.y);

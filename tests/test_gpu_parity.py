@@ -518,3 +518,18 @@ def test_store_leaps_regression_bitwise(gpu, sname, kind, d):
     """the trajectory record on the fp64-MFMA regression kernels (single-slice and d-sliced)"""
     sp = mc.HMC(3, 0.02, storeLeaps=True) if sname == "hmc" else mc.HMCDA(len=0.1, storeLeaps=True, max_leaps=30)
     _store_leaps_case(_glm_model(kind, d), sp, C=40, seed=5 + d, order=0, cap=sp.leaps_cap())
+
+
+@pytest.mark.parametrize("d", [4, 40])
+@pytest.mark.parametrize("eps,nl", [(1e150, 30), (3.0, 250), (3.0, 262)])
+def test_iso_hmc_overflowing_trajectories(gpu, d, eps, nl):
+    """IsoDot HMC takes the half kick as (-x) eps (samplers.hpp trajectory_halfneg); trajectories whose |x| reaches
+    2^1023, where -2x overflows, fall back to the model's gradient: bitwise the oracle's either way.  eps = 3 makes
+    the leapfrog map unstable (|lambda| ~ 16): 250 leapfrogs stay just below the overflow, 262 cross it."""
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
+    r = mc.SerialMC(steps=12)
+    ch = mc.run((m * mc.HMC(nl, eps) * r).batch(70, seed=6))
+    oc = orc.OracleChains(m, mc.HMC(nl, eps), nchains=70, seed=6, order=order_for(d))
+    s, g, acc = oc.run(r)
+    assert_parity(ch, s, g, acc, "hmc")
+    assert ch.task.evals == int(oc.n_evals.sum())
