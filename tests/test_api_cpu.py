@@ -173,3 +173,18 @@ def test_store_leaps_options():
     assert mc.HMCDA(storeLeaps=True, max_leaps=40).leaps_cap() == 40
     assert mc.HMCDA(storeLeaps=True).leaps_cap() == 256
     assert not mc.HMC().storeLeaps
+
+
+def test_bench_traffic_only_from_a_profile_of_the_same_kernel():
+    """bench.py fills roofline.traffic from profiles/traffic.json only when the committed profile is of the same
+    workload AND the same step kernel (a profile of an earlier kernel is stale)"""
+    import importlib
+    import json
+    bench = importlib.import_module("bench")
+    t = json.load(open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "profiles", "traffic.json")))
+    key = next(k for k in t if k.startswith("logistic128|"))
+    assert bench.measured_traffic(key, "glm_mala1<8>")["bytes_per_launch"] == t[key]["traffic_bytes"]
+    assert bench.measured_traffic(key, "glm_mala<8,1>") is None
+    assert bench.measured_traffic("no-such-workload", "lpc_rwm") is None
+    mkey = next(k for k in t if k.startswith("metric|"))
+    assert bench.measured_traffic(mkey, bench.kernel_name(bench.CONFIGS["metric"], 32, "rwm")) is not None
