@@ -20,12 +20,84 @@ __global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* x
     eval_body<LaneChain<NB>, M>(a, xin, lp, g, check);
 }
 
+// RWM for a handful of chains (C <= 64; config 1 is one chain), where one lane per chain leaves the chip idle
+// and each step is a chain of dependent operations: the Philox / Box-Muller work and the accept draw of the
+// next S = 256 / C steps of every chain are spread over the block's 256 threads (thread w: chain w % C, step
+// w / C) and staged in LDS, then lane c of wave 0 runs chain c's S accept steps from there.  rwm_body's
+// operations on the same values (x + RN(z scale), the short-circuit test against det_log(u)), so the chains are
+// bitwise the same.
+constexpr int kLaMaxChains = 64;
+template <int NB, class M, bool US>
+__global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
+    using P = LaneChain<NB, false>;
+    constexpr int NC = P::NC;
+    const StepArgs& s = a.s;
+    const P p(s);                                    // stages the Box-Muller tables (every thread)
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const int C = (int)s.C;
+    const int S = kBlock / C;
+    __shared__ double dz_l[kBlock][NC];
+    __shared__ double lu_l[kBlock];
+    const int w = (int)threadIdx.x;
+    double x[NC], sc[NC];
+    p.load(a.st.x, s.ld, x);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
+    double lp = p.load_scalar(a.st.lp);
+    for (int t0 = 0; t0 < s.nsteps; t0 += S) {
+        const int nb = s.nsteps - t0 < S ? s.nsteps - t0 : S;
+        const int sw = w / C, cw = w - sw * C;
+        if (sw < nb) {                               // RNG of (chain cw, step t0 + sw)
+            const uint32_t chain = s.chain0 + (uint32_t)cw;
+            const uint32_t i = (uint32_t)(s.step_begin + t0 + sw);
+            double z[NC];
+            gen_normals(p, rs, chain, i, z);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) dz_l[w][k] = z[k] * sc[k];           // randn(d) .* scale
+            const u32x4 u = rs.block(chain, i, 0u, TAG_ACCEPT);
+            lu_l[w] = det_log(uniform53(u.x, u.y));                             // log(rand())
+        }
+        __syncthreads();
+        if (w < 64) {                                // wave 0: lane c is chain c
+            for (int j = 0; j < nb; ++j) {
+                const int64_t i = s.step_begin + t0 + j;
+                const int item = p.live ? j * C + w : 0;
+                double xp[NC];
+#pragma unroll
+                for (int k = 0; k < NC; ++k) xp[k] = x[k] + dz_l[item][k];     // pars + randn(d) .* scale
+                bool oos;
+                const double lpp = eval_lp(p, model, xp, oos);
+                const double ratio = lpp - lp;
+                const bool acc = ratio > 0.0 || ratio > lu_l[item];             // RWM.jl:63
+                if (acc) {
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) x[k] = xp[k];
+                    lp = lpp;
+                }
+                int64_t kk;
+                if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+                    p.store_kept(s, kk, x, s.samples);
+                    p.store_bit(s, kk, acc);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    p.store(a.st.x, s.ld, x);
+    p.store_t(a.st.lp, lp);
+    p.count_evals(s, s.nsteps);
+}
+
 template <int NB, bool F, class M>
 static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
     switch (a.sa.kind) {
         case SK_RWM:
-            if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            if (a.s.C <= kLaMaxChains) {
+                if (a.s.scale_uniform) lpc_rwm_la<NB, M, true><<<1, kBlock, 0, st>>>(a);
+                else lpc_rwm_la<NB, M, false><<<1, kBlock, 0, st>>>(a);
+            } else if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
             else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
             break;
         case SK_MALA: lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
