@@ -45,6 +45,11 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
 #pragma unroll
     for (int k = 0; k < NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
     double lp = p.load_scalar(a.st.lp);
+    // kept steps (kept_index) tracked incrementally: i_loc = burnin + 1 + kk thinning <= len; no 64-bit division
+    // on the dependent per-step path
+    const int64_t iloc0 = s.step_begin - s.run_step0;
+    int64_t kk_next = iloc0 > s.burnin + 1 ? (iloc0 - s.burnin - 1 + s.thinning - 1) / s.thinning : 0;
+    int64_t kept_next = s.burnin + 1 + kk_next * s.thinning;
     for (int t0 = 0; t0 < s.nsteps; t0 += S) {
         const int nb = s.nsteps - t0 < S ? s.nsteps - t0 : S;
         const int sw = w / C, cw = w - sw * C;
@@ -75,10 +80,12 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
                     for (int k = 0; k < NC; ++k) x[k] = xp[k];
                     lp = lpp;
                 }
-                int64_t kk;
-                if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
-                    p.store_kept(s, kk, x, s.samples);
-                    p.store_bit(s, kk, acc);
+                const int64_t iloc = i - s.run_step0;
+                if (iloc == kept_next && iloc <= s.len) {                      // SerialMC.jl:49
+                    p.store_kept(s, kk_next, x, s.samples);
+                    p.store_bit(s, kk_next, acc);
+                    kk_next += 1;
+                    kept_next += s.thinning;
                 }
             }
         }
