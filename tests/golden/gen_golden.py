@@ -42,6 +42,8 @@ def _glm_data(kind, d, n):
 
 def make_model(spec):
     kind, d = spec["model"], spec["d"]
+    if kind == "readme":             # README.md:60 mymodel1 = model(v-> -dot(v,v), init=ones(3)); no model scale,
+        return mc.model(mc.IsoNormalDot(), init=np.ones(d))    # so RWM runs its uniform-scale kernel instance
     if kind == "iso":
         return mc.model(mc.IsoNormalDot(), init=np.linspace(0.5, 1.5, d), grad=True,
                         scale=np.linspace(0.8, 1.2, d))
@@ -59,6 +61,7 @@ def make_model(spec):
 
 SAMPLERS = {
     "rwm": lambda glm: mc.RWM(0.05 if glm else 0.6),
+    "rwm01": lambda glm: mc.RWM(0.1),                     # README.md:85 and every BASELINE RWM config
     "mala": lambda glm: mc.MALA(0.002 if glm else 0.4),
     "mala_tuned": lambda glm: mc.MALA(0.01 if glm else 2.0, mc.EmpMCTuner(0.6, adaptStep=3 if glm else 7)),
     "hmc": lambda glm: mc.HMC(3, 0.02) if glm else mc.HMC(4, 0.3),
@@ -70,7 +73,7 @@ SAMPLERS = {
 
 # (name, model spec, sampler, runner (steps, burnin, thinning), chains, seed)
 CASES = []
-for _s in SAMPLERS:
+for _s in ("rwm", "mala", "mala_tuned", "hmc", "hmc_tuned", "hmcda", "ram"):
     CASES.append((f"iso3_{_s}", dict(model="iso", d=3), _s, (40, 5, 3), 8, 101))
     CASES.append((f"normal3_{_s}", dict(model="normal", d=3), _s, (40, 5, 3), 8, 102))
     CASES.append((f"logistic5_{_s}", dict(model="logistic", d=5, n=20), _s, (30, 3, 3), 8, 103))
@@ -82,7 +85,12 @@ for _s in ("rwm", "mala", "hmc", "hmcda"):
 # HMCDA adapts its step only while i < burnin (HMCDA.jl:133): give it a burnin to adapt over
 CASES = [(n, sp, s, (r[0], 15, r[2]) if s == "hmcda" else r, C, sd) for n, sp, s, r, C, sd in CASES]
 CASES.append(("iso32_rwm", dict(model="iso", d=32), "rwm", (40, 5, 3), 64, 108))          # metric shape, small
-CASES.append(("readme_rwm", dict(model="iso", d=3), "rwm", (1000, 100, 1), 1, 1))           # config 1
+# the exact configurations the benchmarks run (uniform scale: the kernel instances bench.py dispatches),
+# at small chain counts that are not multiples of 64
+CASES.append(("readme_rwm", dict(model="readme", d=3), "rwm01", (1000, 100, 1), 1, 1))   # config 1: README.md:60,85
+CASES.append(("readme3_c2_rwm", dict(model="readme", d=3), "rwm01", (100, 10, 10), 200, 1))    # config 2's kernel
+CASES.append(("metric32_rwm", dict(model="readme", d=32), "rwm01", (100, 10, 10), 200, 1))     # the metric's kernel
+CASES.append(("readme_c37_rwm", dict(model="readme", d=3), "rwm01", (300, 30, 7), 37, 3))      # look-ahead kernel
 
 
 def case_sampler(spec, sname):

@@ -1,0 +1,155 @@
+"""The exact kernel instances the benchmarks dispatch, parity-tested on the GPU.
+
+bench.py's RWM workloads use README.md:60's model (`-dot(v,v)`, init `ones(d)`, no model scale) under
+`RWM(0.1)` (README.md:85): every coordinate's effective scale `model.scale .* sampler.scale` (RWM.jl:52) is the
+same, so the runtime launches the uniform-scale specialisations (`scale1` in a scalar register).  These tests
+run those workloads' own configurations, read back which step kernel ran (`mcmc_chains_step_kernel`), and
+compare the HIP results with the oracle bit for bit:
+
+- config 2 (d=3) -> `lpc_rwm<1, false, IsoDot, true>`; the metric (d=32) -> `lpc_rwm<8, true, IsoDot, true>`;
+- config 1 (one chain) and C <= 64 -> the look-ahead kernel `lpc_rwm_la`, also across launches
+  (`steps_per_launch`) and continued runs, where a launch starts mid-way through the kept range;
+- the metric at its full size: 2^20 chains, d=32, SerialMC(1000, 100, 10) with device-resident outputs,
+  checked bitwise on 4 096 chains spread over the batch and on every chain's accept bits' statistics.
+"""
+import numpy as np
+import pytest
+
+import mcmchip as mc
+import oracle_ref as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _readme_model(d):
+    return mc.model(mc.IsoNormalDot(), init=np.ones(d))          # README.md:60 (d = 3), bench.py's RWM model
+
+
+def _check(chain, s_ref, acc_ref):
+    acc = chain.diagnostics["accept"].T
+    assert np.array_equal(acc, acc_ref.astype(bool)), f"accept bits differ in {np.count_nonzero(acc != acc_ref)}"
+    np.testing.assert_allclose(chain._samples, s_ref, rtol=1e-10, atol=0)      # north_star tolerance
+    assert np.array_equal(chain._samples.view(np.uint64), s_ref.view(np.uint64)), "samples not bit-identical"
+
+
+@pytest.mark.parametrize("d,C,kernel", [
+    (3, 1000, "lpc_rwm<1, false, IsoDot, true>"),      # config 2's instance
+    (32, 1000, "lpc_rwm<8, true, IsoDot, true>"),      # the metric's instance
+    (4, 300, "lpc_rwm<1, true, IsoDot, true>"),
+    (17, 130, "lpc_rwm<5, false, IsoDot, true>"),
+    (32, 65, "lpc_rwm<8, true, IsoDot, true>"),        # one chain past the look-ahead limit
+])
+def test_uniform_scale_rwm_instances(gpu, d, C, kernel):
+    m = _readme_model(d)
+    r = mc.SerialMC(steps=200, burnin=20, thinning=10)
+    t = (m * mc.RWM(0.1) * r).batch(C, seed=1)
+    chain = mc.run(t)
+    assert t.step_kernel == kernel
+    oc = orc.OracleChains(m, mc.RWM(0.1), nchains=C, seed=1)
+    s_ref, _, acc_ref = oc.run(r)
+    _check(chain, s_ref, acc_ref)
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+
+
+def test_nonuniform_scale_takes_the_generic_instance(gpu):
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(32), scale=np.linspace(0.8, 1.2, 32))
+    t = (m * mc.RWM(0.1) * mc.SerialMC(steps=10)).batch(128, seed=1)
+    mc.run(t)
+    assert t.step_kernel == "lpc_rwm<8, true, IsoDot, false>"
+
+
+@pytest.mark.parametrize("uniform", [True, False])
+@pytest.mark.parametrize("spl", [0, 1, 7])
+@pytest.mark.parametrize("C", [1, 37, 64])
+def test_lookahead_rwm_across_launches_and_runs(gpu, C, spl, uniform):
+    """lpc_rwm_la (C <= 64): with steps_per_launch 1 or 7 and a continued run, launches begin inside the kept
+    range (lpc_impl.hpp: the kept-step counter restarts from step_begin - run_step0 > burnin + 1)."""
+    d = 3
+    m = (_readme_model(d) if uniform else
+         mc.model(mc.IsoNormalDot(), init=np.ones(d), scale=np.array([0.8, 1.0, 1.3])))
+    r = mc.SerialMC(steps=150, burnin=20, thinning=7)
+    t = (m * mc.RWM(0.1) * r).batch(C, seed=3, steps_per_launch=spl)
+    c1 = mc.run(t)
+    c2 = mc.run(c1)                                               # runners.jl:14: the same chains continue
+    assert t.step_kernel == f"lpc_rwm_la<1, IsoDot, {'true' if uniform else 'false'}>"
+    oc = orc.OracleChains(m, mc.RWM(0.1), nchains=C, seed=3)
+    s1, _, a1 = oc.run(r)
+    s2, _, a2 = oc.run(r)
+    _check(c1, s1, a1)
+    _check(c2, s2, a2)
+    assert t.steps_done == 300
+
+
+def test_readme_config1_instance(gpu):
+    """config 1 exactly: README.md:60,85 run(mymodel1, RWM(0.1), SerialMC(steps=1000, burnin=100)), one chain."""
+    m1 = _readme_model(3)
+    t = (m1 * mc.RWM(0.1) * mc.SerialMC(steps=1000, burnin=100)).batch(1, seed=1)
+    ch = mc.run(t)
+    assert t.step_kernel == "lpc_rwm_la<1, IsoDot, true>"
+    oc = orc.OracleChains(m1, mc.RWM(0.1), nchains=1, seed=1)
+    s, _, acc = oc.run(mc.SerialMC(steps=1000, burnin=100))
+    _check(ch, s, acc)
+    assert ch.samples.shape == (1, 900, 3)
+
+
+def test_full_size_metric_run(gpu):
+    """The metric workload at its full size (BASELINE.json metric; bench.py --config metric --steps 1000):
+    2^20 chains, d=32, init ones(32), RWM(0.1), SerialMC(steps=1000, burnin=100, thinning=10), seed 1, outputs
+    resident on the device.  4 096 chains -- 64 blocks of 64 spread over the batch, the first and last chain
+    included -- are compared bit for bit with the oracle (the oracle keys its stream by global chain id, so a
+    block at chain_offset k is exactly chains k..k+63 of the full run).  Every chain: the accept fraction and
+    the final moments agree with the subset's within their sampling error."""
+    import ctypes as ct
+    import torch
+    from mcmchip import _lib
+
+    d, C = 32, 1 << 20
+    m = _readme_model(d)
+    r = mc.SerialMC(steps=1000, burnin=100, thinning=10)
+    t = (m * mc.RWM(0.1) * r).batch(C, seed=1)
+    h = t.handle()
+    lib = _lib.load()
+    nk = len(r.r)
+    dev = torch.device("cuda", 0)
+    samples = torch.empty((nk, d, C), dtype=torch.float64, device=dev)
+    bits = torch.empty((nk, C // 64), dtype=torch.int64, device=dev)
+    fx = torch.empty((d, C), dtype=torch.float64, device=dev)
+    out = _lib.Outputs()
+    out.samples, out.accept_bits, out.final_x = samples.data_ptr(), bits.data_ptr(), fx.data_ptr()
+    out.on_device = 1
+    cfg = r.cfg()
+    _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
+    torch.cuda.synchronize(dev)
+    assert t.step_kernel == "lpc_rwm<8, true, IsoDot, true>"
+    assert out.nkept == 90
+
+    starts = np.unique(np.linspace(0, C - 64, 64).astype(np.int64) // 64 * 64)
+    assert len(starts) == 64 and starts[0] == 0 and starts[-1] == C - 64
+    acc_sub = []
+    for c0 in starts:
+        oc = orc.OracleChains(m, mc.RWM(0.1), nchains=64, seed=1, chain_offset=int(c0))
+        s_ref, _, a_ref = oc.run(r)
+        s_gpu = samples[:, :, c0:c0 + 64].cpu().numpy()
+        assert np.array_equal(s_gpu.view(np.uint64), s_ref.view(np.uint64)), f"samples of chains {c0}.. differ"
+        w = bits[:, c0 // 64].cpu().numpy().view(np.uint64)
+        a_gpu = ((w[:, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(np.uint8)
+        assert np.array_equal(a_gpu, a_ref), f"accept bits of chains {c0}.. differ"
+        assert np.array_equal(fx[:, c0:c0 + 64].cpu().numpy(), oc.x)
+        acc_sub.append(a_ref)
+    acc_sub = np.concatenate(acc_sub, axis=1)
+    # every chain: accept fraction per kept step and overall, from the ballot words
+    b = bits.view(torch.uint8)
+    table = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.float64, device=dev)
+    pop = table[b.long()].sum(dim=1)
+    rate_all = float(pop.sum()) / (nk * C)
+    rate_sub = acc_sub.mean()
+    se = np.sqrt(rate_sub * (1 - rate_sub) / acc_sub.size)
+    assert abs(rate_all - rate_sub) < 6 * se + 1e-3, (rate_all, rate_sub)
+    # final state moments over all chains vs the 4 096-chain subset (chains are i.i.d. replicas)
+    mean_all = fx.mean(dim=1).cpu().numpy()
+    var_all = fx.var(dim=1).cpu().numpy()
+    sub = np.concatenate([fx[:, c0:c0 + 64].cpu().numpy() for c0 in starts], axis=1)
+    se_mean = np.sqrt(sub.var(axis=1) / sub.shape[1])
+    assert np.all(np.abs(mean_all - sub.mean(axis=1)) < 6 * se_mean)
+    assert np.all(np.abs(var_all / sub.var(axis=1) - 1) < 6 * np.sqrt(2 / sub.shape[1]))
+    assert bool(torch.isfinite(samples).all())
