@@ -74,6 +74,7 @@ def parse():
     p.add_argument("--spl", type=int, default=-1, help="steps per launch (0: whole run in one launch; "
                                                        "-1: default of the library)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-ess", action="store_true", help="skip the ESS/sec leg")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--strong", action="store_true", help="fixed total chains (--chains) split over ranks")
     p.add_argument("--pcie", action="store_true", help="also time one run with host output buffers (kept samples "
@@ -154,14 +155,41 @@ def measured_traffic(wkey, kname):
             "source": e["source"], "unit": "B"}
 
 
+def host_cpus():
+    """The host cores this process may use: its CPU affinity set, capped by the cgroup's CPU quota when one is
+    set (a GPU box shows every CPU of the machine in nproc / os.cpu_count() but grants a share of them), plus
+    the CPU model (lscpu's "Model name", read from /proc/cpuinfo)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"usable": usable, "nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota, "model": model}
+
+
 def cpu_baseline(model, sampler, seconds, C=4096):
-    """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample; a one-chain
-    workload (config 1) is timed as one chain on one core."""
+    """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample, on every host
+    core this process may use (host_cpus); a one-chain workload (config 1) is timed as one chain on one core."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref as orc
     import mcmchip as mc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1, C))
+    host = host_cpus()
+    threads = max(1, min(host["usable"], C))
     # double the sample until one run takes about `seconds` / 2 (state set-up excluded); that last run is the
     # sample -- same runner shape (burnin = steps/10, thinning 10) at every size, so an adaptive sampler's
     # cost per step is measured as configured, and the wall time stays bounded (< ~2 x seconds in total)
@@ -175,13 +203,33 @@ def cpu_baseline(model, sampler, seconds, C=4096):
             break
         steps *= 2 if dt > seconds / 16 else 4
     return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
+            "host": host,
             "sample": f"{C} chains x {steps} steps of the same workload on the host ({dt:.1f} s), "
-                      f"oracle/oracle.c OpenMP over chains; chains are independent, so the rate is per chain-step"}
+                      f"oracle/oracle.c OpenMP over {threads} threads (every usable core; chains are independent, "
+                      f"so the rate is per chain-step)"}
+
+
+def spawn_workers(args, argv):
+    """`--gpus N` (N > 1) started as a plain process (no torchrun, WORLD_SIZE unset): re-launch this same command
+    under torch.distributed.run with N processes, one per GPU, and return its exit code.  Runs before anything
+    touches the GPU, and starts the workers as a child process (never an exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_workers(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one process per GPU is required")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -260,24 +308,59 @@ def main():
     value = total_chains * K / T
 
     # ESS/sec: sum over chains of min over parameters of the IMSE ESS of the kept
-    # samples, per second of sampling; computed on the device after the timed region, timed apart
+    # samples, per second of sampling; computed on the device after the timed region, timed apart.  When the
+    # timed run keeps fewer than 20 samples per chain (the IMSE/IPSE estimators need a usable number of lags;
+    # e.g. --steps 20 keeps 2), a separate run of the configuration's own SerialMC (BASELINE: 1000 steps,
+    # burnin 100, thinning 10) on fresh chains of the same workload is sampled and timed for it.
     ess_line = None
-    if nkept >= 20:                     # the IMSE/IPSE estimators need a usable number of lags
-        torch.cuda.synchronize(dev)
-        te = time.perf_counter()
-        ess = mc.stats.ess_device(samples, "imse")
-        # a chain that never moved has a 0/0 ESS (var.jl gives NaN), and an antithetic series whose first
-        # Geyer pair is <= 0 gets a negative IMSE variance (var.jl:53-57, m = 0): both count as 0 samples
-        ess_min_sum = torch.nan_to_num(ess, nan=0.0).clamp(min=0.0).min(dim=0).values.sum()
-        torch.cuda.synchronize(dev)
-        ess_s = time.perf_counter() - te
-        if dist is not None:
-            ess_min_sum = ess_min_sum.to(red_dev)
-            dist.all_reduce(ess_min_sum, op=dist.ReduceOp.SUM)
-        ess_line = {"ess_per_sec": float(ess_min_sum) / T, "vtype": "imse", "kept_per_chain": nkept,
-                    "sum_min_ess": float(ess_min_sum), "ess_compute_s": ess_s,
-                    "note": "sum_c min_j ESS_cj (ess.jl:6-10, Geyer IMSE; NaN or negative estimates count as 0) / "
-                            "sampling seconds; ESS on the GPU (kernels/stats.hip), outside the timed region"}
+    if not args.no_ess:
+        leg = "timed run"
+        e_samples, e_T, e_nkept = samples, T, nkept
+        if nkept < 20:
+            es, eb, et = cfg0["steps"], cfg0["steps"] // 10, cfg0["thinning"]
+            er = mc.SerialMC(steps=es, burnin=eb, thinning=et)
+            e_nkept = len(er.r)
+            etask = mc.MCMCTask(model, sampler, er, nchains=C, seed=2, device=local, chain_offset=rank * C,
+                                steps_per_launch=max(args.spl, 0))
+            e_samples = torch.empty((e_nkept, d, C), dtype=torch.float64, device=dev)
+            e_grads = torch.empty((e_nkept, d, C), dtype=torch.float64, device=dev) if grad_sampler else None
+            eout = _lib.Outputs()
+            eout.samples = e_samples.data_ptr()
+            eout.gradients = e_grads.data_ptr() if e_grads is not None else None
+            eout.on_device = 1
+            eh = etask.handle()
+            _lib.check(lib.mcmc_chains_reserve_outputs(eh, e_nkept, 1))
+            ecfg = er.cfg()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            _lib.check(lib.mcmc_run_serialmc(eh, ct.byref(ecfg), ct.byref(eout)))
+            torch.cuda.synchronize(dev)
+            e_T = time.perf_counter() - t0
+            del e_grads
+            leg = (f"separate run: SerialMC(steps={es}, burnin={eb}, thinning={et}) of the same workload, seed 2 "
+                   f"(the timed run keeps {nkept} < 20 samples per chain)")
+        if e_nkept >= 20:
+            torch.cuda.synchronize(dev)
+            te = time.perf_counter()
+            ess = mc.stats.ess_device(e_samples, "imse")
+            # a chain that never moved has a 0/0 ESS (var.jl gives NaN), and an antithetic series whose first
+            # Geyer pair is <= 0 gets a negative IMSE variance (var.jl:53-57, m = 0): both count as 0 samples
+            ess_min_sum = torch.nan_to_num(ess, nan=0.0).clamp(min=0.0).min(dim=0).values.sum()
+            torch.cuda.synchronize(dev)
+            ess_s = time.perf_counter() - te
+            if dist is not None:
+                esum = ess_min_sum.double().reshape(1).to(red_dev)
+                tmax = torch.tensor([e_T], dtype=torch.float64, device=red_dev)
+                dist.all_reduce(esum, op=dist.ReduceOp.SUM)
+                dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+                ess_min_sum, e_T = esum[0], float(tmax[0])
+            ess_line = {"ess_per_sec": float(ess_min_sum) / e_T, "vtype": "imse", "kept_per_chain": e_nkept,
+                        "sum_min_ess": float(ess_min_sum), "sampling_s": e_T, "ess_compute_s": ess_s, "leg": leg,
+                        "note": "sum_c min_j ESS_cj (ess.jl:6-10, Geyer IMSE; NaN or negative estimates count as "
+                                "0) / sampling seconds of that run; ESS on the GPU (kernels/stats.hip), outside "
+                                "the timed region"}
+        if e_samples is not samples:
+            del e_samples
 
     pcie = None
     if args.pcie:

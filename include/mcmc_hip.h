@@ -198,6 +198,11 @@ int mcmc_chains_reserve_outputs(mcmc_chains* chains, int64_t nkept, int32_t on_d
 /* kernel launches a run of len steps takes (steps per launch as set, capped by kernels that fuse a
  * bounded number of steps); for timing per launch. */
 int mcmc_chains_launches(mcmc_chains* chains, int64_t len, int64_t* launches);
+/* the step kernel instance the last mcmc_run_serialmc launched, e.g. "lpc_rwm<8, true, IsoDot, true>"
+ * (the template instance rocprofv3 names, without the namespace), NUL-terminated into buf[cap];
+ * "" before the first run.  No reference counterpart: lets tests and benchmarks check which
+ * specialisation ran. */
+int mcmc_chains_step_kernel(mcmc_chains* chains, char* buf, int64_t cap);
 
 /* storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117; HMC and HMCDA only).  The next mcmc_run_serialmc records, for
  * every kept step, the states of its trajectory -- leap 0 = state0 after update!, leap l = the state after

@@ -14,6 +14,12 @@ struct KernelArgs {
 };
 }  // namespace mcmc
 
+// The step kernel a launch function dispatched, as "family<template arguments>" (the instance name rocprofv3
+// shows, without the namespace): the launch functions record it, mcmc_chains_step_kernel reports it (tests and
+// bench.py check which instance ran).  Host-side, thread-local; printf-style.
+void mcmc_note_step_kernel(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+const char* mcmc_last_step_kernel();
+
 // lane-per-chain kernels (d <= 32), state [d][ld]
 hipError_t mcmc_launch_lpc_step(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_launch_lpc_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,

@@ -38,6 +38,17 @@ static int fail(int code, const std::string& msg) {
     } while (0)
 
 extern "C" const char* mcmc_last_error(void) { return g_err.c_str(); }
+
+// the step kernel instance the last launch function on this thread dispatched (kernels_api.hpp)
+#include <cstdarg>
+static thread_local char g_step_kernel[160];
+void mcmc_note_step_kernel(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_step_kernel, sizeof g_step_kernel, fmt, ap);
+    va_end(ap);
+}
+const char* mcmc_last_step_kernel() { return g_step_kernel; }
 extern "C" int mcmc_abi_version(void) { return MCMC_ABI_VERSION; }
 extern "C" int mcmc_device_count(int* count) {
     if (!count) return fail(MCMC_E_INVALID_ARG, "count is NULL");
@@ -99,6 +110,7 @@ struct mcmc_chains {
     double *h_lpars = nullptr, *h_lgrads = nullptr, *h_lmom = nullptr, *h_llp = nullptr, *h_lH = nullptr;
     int32_t* h_lnl = nullptr;
     DevBuf leap_buf;
+    std::string step_kernel;         // the step kernel instance the last run launched
 };
 
 // Transfers are ordered on the context's (non-blocking) stream, after every kernel queued there,
@@ -731,6 +743,12 @@ extern "C" int mcmc_chains_steps_done(mcmc_chains* c, int64_t* steps) {
     return MCMC_OK;
 }
 
+extern "C" int mcmc_chains_step_kernel(mcmc_chains* c, char* buf, int64_t cap) {
+    if (!c || !buf || cap < 1) return fail(MCMC_E_INVALID_ARG, "bad argument");
+    std::snprintf(buf, (size_t)cap, "%s", c->step_kernel.c_str());
+    return MCMC_OK;
+}
+
 extern "C" int mcmc_chains_set_steps_per_launch(mcmc_chains* c, int64_t spl) {
     if (!c || spl < 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
     c->spl = spl;
@@ -921,7 +939,9 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
             lr.nl = (int32_t*)(dl + 3 * nk * lsz + 2 * nk * lsc) + (size_t)kk * (size_t)C;
             HIP_TRY(launch_record(L, a, lr, st));
         }
+        g_step_kernel[0] = 0;
         HIP_TRY(launch_step(L, a, st));
+        c->step_kernel = g_step_kernel;
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     if (L == LAYOUT_WPC) {

@@ -1248,6 +1248,17 @@ static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hip
     using namespace mcmc;
     constexpr int B = glm_block<NW>();
     switch (a.sa.kind) {
+        case SK_RWM: mcmc_note_step_kernel("glm_rwm<%d, %d>", NM, NW); break;
+        case SK_MALA:
+            if (NW == 1) mcmc_note_step_kernel("glm_mala1<%d>", NM);
+            else mcmc_note_step_kernel("glm_mala<%d, %d>", NM, NW);
+            break;
+        case SK_HMC: mcmc_note_step_kernel("glm_hmc<%d, %d, false>", NM, NW); break;
+        case SK_HMCDA: mcmc_note_step_kernel("glm_hmc<%d, %d, true>", NM, NW); break;
+        case SK_RAM: mcmc_note_step_kernel("glm_ram<%d, %d>", NM, NW); break;
+        default: break;
+    }
+    switch (a.sa.kind) {
         case SK_RWM: glm_rwm<NM, NW><<<grid, B, lds, st>>>(a); break;
         case SK_MALA:
             if constexpr (NW == 1) return mcmc_launch_glm_mala1(NM, a, lds, grid, st);   // glm_mala1.hip

@@ -99,17 +99,32 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
 template <int NB, bool F, class M>
 static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    const char* b = F ? "true" : "false";
+    const char* us = a.s.scale_uniform ? "true" : "false";
     switch (a.sa.kind) {
         case SK_RWM:
             if (a.s.C <= kLaMaxChains) {
+                mcmc_note_step_kernel("lpc_rwm_la<%d, %s, %s>", NB, M::kName, us);
                 if (a.s.scale_uniform) lpc_rwm_la<NB, M, true><<<1, kBlock, 0, st>>>(a);
                 else lpc_rwm_la<NB, M, false><<<1, kBlock, 0, st>>>(a);
-            } else if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+                break;
+            }
+            mcmc_note_step_kernel("lpc_rwm<%d, %s, %s, %s>", NB, b, M::kName, us);
+            if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
             else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
             break;
-        case SK_MALA: lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_HMC: lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a); break;
-        case SK_HMCDA: lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a); break;
+        case SK_MALA:
+            mcmc_note_step_kernel("lpc_mala<%d, %s, %s>", NB, b, M::kName);
+            lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a);
+            break;
+        case SK_HMC:
+            mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, false>", NB, b, M::kName);
+            lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            break;
+        case SK_HMCDA:
+            mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, true>", NB, b, M::kName);
+            lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -201,6 +216,7 @@ __global__ __launch_bounds__(kBlock, NB <= 4 ? 2 : 1) void lpc_ram(KernelArgs a)
 template <class M>
 static hipError_t lpc_ram_step(const KernelArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    mcmc_note_step_kernel("lpc_ram<%d, %s>", (a.s.d + 3) / 4, M::kName);
     switch ((a.s.d + 3) / 4) {
         case 1: lpc_ram<1, M><<<grid, kBlock, 0, st>>>(a); break;
         case 2: lpc_ram<2, M><<<grid, kBlock, 0, st>>>(a); break;

@@ -25,6 +25,10 @@ __global__ __launch_bounds__(kBlock) void wpc_eval(KernelArgs a, const double* x
 template <int NB, bool F, class M>
 static hipError_t wpc_launch_model(const KernelArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    static const char* const fam[] = {"", "wpc_rwm<%d, %s, %s>", "wpc_mala<%d, %s, %s>", "wpc_hmc<%d, %s, %s, false>",
+                                      "wpc_hmc<%d, %s, %s, true>"};
+    if (a.sa.kind >= SK_RWM && a.sa.kind <= SK_HMCDA)
+        mcmc_note_step_kernel(fam[a.sa.kind], NB, F ? "true" : "false", M::kName);
     switch (a.sa.kind) {
         case SK_RWM: wpc_rwm<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;
         case SK_MALA: wpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a); break;

@@ -34,6 +34,7 @@ constexpr double kLog2Pi = 0x1.d67f1c864beb5p+0;   // log(2*pi) rounded
 constexpr double kTwoPi = 0x1.921fb54442d18p+2;    // 2*pi rounded (Julia 2*pi)
 
 struct IsoDot {
+    static constexpr const char* kName = "IsoDot";
     static constexpr bool kLLAcc = false;
     // 0.5 * grad(v) = 0.5 * (-2 v) is -v exactly while |v| < 2^1023 (samplers.hpp trajectory_halfneg)
     static constexpr bool kHalfGradNeg = true;
@@ -44,6 +45,7 @@ struct IsoDot {
 };
 
 struct NormalDSL {
+    static constexpr const char* kName = "NormalDSL";
     static constexpr bool kLLAcc = true;
     static constexpr bool kHalfGradNeg = false;
     double mu, sigma, logsig, s2;
@@ -60,6 +62,7 @@ struct NormalDSL {
 };
 
 struct AbsNormalDSL {
+    static constexpr const char* kName = "AbsNormalDSL";
     static constexpr bool kLLAcc = true;
     static constexpr bool kHalfGradNeg = false;
     double mu, sigma, logsig, s2;
@@ -86,6 +89,7 @@ struct AbsNormalDSL {
 // the host (restated by oracle/oracle.c orc_dist_const).  The distribution is uniform over a launch:
 // the switch is a scalar branch.
 struct DistDSL {
+    static constexpr const char* kName = "DistDSL";
     static constexpr bool kLLAcc = true;
     static constexpr bool kHalfGradNeg = false;
     int32_t dist;

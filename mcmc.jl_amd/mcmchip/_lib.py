@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done", "mcmc_chains_evals",
     "mcmc_chains_ram_factor",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients", "mcmc_chains_reserve_outputs",
-    "mcmc_chains_launches", "mcmc_chains_store_leaps", "mcmc_run_serialmc", "mcmc_seqmc_validate", "mcmc_run_seqmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
+    "mcmc_chains_launches", "mcmc_chains_step_kernel", "mcmc_chains_store_leaps", "mcmc_run_serialmc", "mcmc_seqmc_validate", "mcmc_run_seqmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox", "mcmc_debug_mfma_f64",
 )
 
 
@@ -145,6 +145,7 @@ def load() -> ct.CDLL:
         "mcmc_chains_set_store_gradients": (ct.c_int, [P, i32]),
         "mcmc_chains_reserve_outputs": (ct.c_int, [P, i64, i32]),
         "mcmc_chains_launches": (ct.c_int, [P, i64, ct.POINTER(i64)]),
+        "mcmc_chains_step_kernel": (ct.c_int, [P, ct.c_char_p, i64]),
         "mcmc_chains_store_leaps": (ct.c_int, [P, i64, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p,
                                                ct.c_void_p, ct.c_void_p]),
         "mcmc_run_serialmc": (ct.c_int, [P, ct.POINTER(RunnerCfg), ct.POINTER(Outputs)]),

@@ -503,6 +503,14 @@ class MCMCTask:
         check(_lib.load().mcmc_chains_evals(self._h, ct.byref(v)))
         return v.value
 
+    @property
+    def step_kernel(self) -> str:
+        """The step kernel instance the last run launched (mcmc_chains_step_kernel), e.g.
+        "lpc_rwm<8, true, IsoDot, true>"; "" before the first run."""
+        buf = ct.create_string_buffer(160)
+        check(_lib.load().mcmc_chains_step_kernel(self.handle(), buf, len(buf)))
+        return buf.value.decode()
+
     def ram_factor(self) -> np.ndarray:
         """RAM: the current jump factor S of every chain as [nchains][d][d] lower-triangular matrices."""
         if self._h is None:
