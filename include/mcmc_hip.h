@@ -180,10 +180,10 @@ int mcmc_chains_reset(mcmc_chains* chains);
 /* steps consumed so far (the sampler's own loop counter i). */
 int mcmc_chains_steps_done(mcmc_chains* chains, int64_t* steps);
 /* log-target evaluations (with gradient for MALA/HMC/HMCDA) summed over all chains since
- * create/reset: steps x C for RWM/MALA, the leapfrog count for HMC/HMCDA (HMC.jl:219-228),
+ * create/reset: steps x C for RWM/MALA, the leapfrog count for HMC/HMCDA (HMC.jl:93-102),
  * whose trajectory length varies per chain under HMCDA / EmpMCTuner. */
 int mcmc_chains_evals(mcmc_chains* chains, int64_t* evals);
-/* RAM: the current jump factor S of every chain (RAM.jl:55, :81), lower triangle packed by rows:
+/* RAM: the current jump factor S of every chain (RAM.jl:55, :78), lower triangle packed by rows:
  * element (r, c), c <= r, of chain k at S[(r(r+1)/2 + c) * nchains + k]; host buffer of
  * d(d+1)/2 * nchains doubles.  MCMC_E_INVALID_ARG for other samplers. */
 int mcmc_chains_ram_factor(mcmc_chains* chains, double* S);

@@ -564,7 +564,7 @@ static int init_state(mcmc_chains* c) {
     }
     if (sa.kind == SK_HMCDA) {
         // initializeHMCDAStep returns 1 for every chain: state0.H is still NaN when it runs
-        // (HMC.jl:214 ctor, HMCDA.jl:86-92), so p = NaN, a = -1 and the while loop never runs.
+        // (HMC.jl:88 ctor, HMCDA.jl:86-92), so p = NaN, a = -1 and the while loop never runs.
         HIP_TRY(mcmc_fill_f64(c->st.t_step, c->C, 1.0, st));
         HIP_TRY(mcmc_fill_f64(c->st.t_bar, c->C, 1.0, st));     // dualLeapStep = 1.
         HIP_TRY(mcmc_fill_f64(c->st.t_h, c->C, 0.0, st));       // dualH = 0.

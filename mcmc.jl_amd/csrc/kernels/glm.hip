@@ -699,7 +699,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_rwm(GlmArgs a) {
     glm_count_evals(a, p, s.nsteps);
 }
 
-// RAM (RAM.jl:56-82) for d <= 32 (one d-slice, NW = 1), the factor padded to DF = 16 NM (ram.hpp).
+// RAM (RAM.jl:55-78) for d <= 32 (one d-slice, NW = 1), the factor padded to DF = 16 NM (ram.hpp).
 // Row r of S belongs to the lane that owns coordinate r (own_coord): it forms u[r] = (S z)[r] from the
 // full normal vector (every lane of the chain draws all DF/4 blocks), keeps it across the evaluation,
 // and after the accept updates its rows of every column k; the pivot u[k] comes from its owner by a
@@ -1120,7 +1120,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
             pa = __builtin_fmin(1.0, det_exp(H0 - H));              // HMCDA.jl:120
             acc = u < pa;
         } else {
-            acc = u < det_exp(H0 - H);                              // HMC.jl:280
+            acc = u < det_exp(H0 - H);                              // HMC.jl:154
         }
         if (acc) {
             glm_store<NM>(a, p, a.st.x, s.ld, x);

@@ -1,4 +1,4 @@
-// ram.hpp -- the jump-factor arithmetic of the robust adaptive Metropolis sampler (RAM.jl:56-82),
+// ram.hpp -- the jump-factor arithmetic of the robust adaptive Metropolis sampler (RAM.jl:55-78),
 // shared by the lane-per-chain (samplers.hpp ram_body) and regression (glm.hip glm_ram) kernels.
 //
 // Storage.  S is the chain's d x d lower-triangular jump factor, kept in HBM as packed rows padded to
@@ -21,7 +21,7 @@
 
 namespace mcmc {
 
-// eta * (min(1, exp(ratio)) - rate), eta = min(1, d i^(-2/3))   (RAM.jl:77-79)
+// eta * (min(1, exp(ratio)) - rate), eta = min(1, d i^(-2/3))   (RAM.jl:74-76)
 __device__ __forceinline__ double ram_alpha(int64_t i, int d, double ratio, double rate) {
     const double eta = __builtin_fmin(1.0, (double)d * det_exp((-2.0 / 3.0) * det_log((double)i)));
     return eta * (__builtin_fmin(1.0, det_exp(ratio)) - rate);

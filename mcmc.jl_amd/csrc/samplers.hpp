@@ -19,7 +19,7 @@
 // Per step (reference file:line for each sampler):
 //   RWM    RWM.jl:58-71      x' = x + randn .* scale; accept iff r > 0 || r > log(rand())
 //   MALA   MALA.jl:89-125    Langevin proposal, forward/backward densities, EmpMCTuner
-//   HMC    HMC.jl:252-299    L leapfrogs (HMC.jl:219-228), accept iff rand() < exp(H0 - H)
+//   HMC    HMC.jl:126-173    L leapfrogs (HMC.jl:93-102), accept iff rand() < exp(H0 - H)
 //   HMCDA  HMCDA.jl:97-142   nLeaps = max(1, round(len/eps)), p = min(1, exp(H0-H)),
 //                            dual averaging while i < burnin
 #pragma once
@@ -400,7 +400,7 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
 }
 
 // ------------------------------------------------------------------ HMC / HMCDA
-// nl leapfrogs from (x, m) (HMC.jl:219-228); the start point is in support.
+// nl leapfrogs from (x, m) (HMC.jl:93-102); the start point is in support.
 // Two restructurings, both bitwise neutral:
 //  * the half kick (0.5 g) eps at a point is computed once and used by the closing half kick of one
 //    leapfrog and the opening one of the next (the same x, the same oos flag) -- when the chain's
@@ -532,7 +532,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             pa = __builtin_fmin(1.0, det_exp(H0 - H));          // HMCDA.jl:120 (Julia 0.2 min: NaN-ignoring)
             acc = u < pa;
         } else {
-            acc = u < det_exp(H0 - H);                          // HMC.jl:280
+            acc = u < det_exp(H0 - H);                          // HMC.jl:154
         }
         if (acc) {
 #pragma unroll
@@ -562,7 +562,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             } else {
                 eps = eps_bar;                                  // HMCDA.jl:140
             }
-        } else if (tuned && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // HMC.jl:293-295
+        } else if (tuned && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // HMC.jl:167-169
             eps = eps * tune_factor(n_acc, n_prop, sa.target_rate);
             double nlf = __builtin_ceil(sa.target_path / eps);
             if (nlf > (double)sa.max_step) nlf = (double)sa.max_step;
@@ -648,8 +648,8 @@ __device__ __forceinline__ void hmc_record_body(const KernelArgs& a, const LeapR
 }
 
 // ------------------------------------------------------------------ RAM
-// Robust adaptive Metropolis (RAM.jl:39-83), lane per chain.  x' = x + S z, RWM accept, then the
-// jump factor S (packed rows in HBM, ram.hpp) takes the rank-1 update of RAM.jl:77-81.
+// Robust adaptive Metropolis (RAM.jl:41-79), lane per chain.  x' = x + S z, RWM accept, then the
+// jump factor S (packed rows in HBM, ram.hpp) takes the rank-1 update of RAM.jl:74-78.
 template <class P, class M>
 __device__ __forceinline__ void ram_body(const KernelArgs& a) {
     const StepArgs& s = a.s;

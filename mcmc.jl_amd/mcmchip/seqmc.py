@@ -101,7 +101,7 @@ def run_seqmc(targets: Sequence[MCMCTask], particles=None, seed: int = 1, device
 
 
 def resume_seqmc(targets: Sequence[MCMCTask], steps: int = 100, **kw) -> SeqMCChain:
-    """resume_seqmc (SeqMC.jl:126-129): the same targets, a new SeqMC(steps, trigger) run."""
+    """resume_seqmc (SeqMC.jl:125-128): the same targets, a new SeqMC(steps, trigger) run."""
     trig = targets[-1].runner.trigger
     new = [MCMCTask(t.model, t.sampler, SeqMC(steps=steps, trigger=trig)) for t in targets]
     return run_seqmc(new, **kw)

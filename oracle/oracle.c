@@ -418,7 +418,7 @@ static int orc_mh_short_circuit(uint64_t seed, uint32_t chain, uint32_t step, do
     return ratio > orc_log(orc_accept_uniform(seed, chain, step));
 }
 
-/* nl leapfrogs (HMC.jl:219-228) from (x, mom, g); returns the final lp */
+/* nl leapfrogs (HMC.jl:93-102) from (x, mom, g); returns the final lp */
 static double orc_trajectory(const orc_model* m, double eps, int64_t nl, double* x, double* mom, double* g,
                              double lp, double* tmp, int order) {
     const int d = m->d;
@@ -431,7 +431,7 @@ static double orc_trajectory(const orc_model* m, double eps, int64_t nl, double*
     return lp;
 }
 
-/* RAM scale tuning (RAM.jl:77-81) on the packed factor Lc (element (r, c) at Lc[(r(r+1)/2 + c) * C]).
+/* RAM scale tuning (RAM.jl:74-78) on the packed factor Lc (element (r, c) at Lc[(r(r+1)/2 + c) * C]).
    The reference sets S = chol(S (I + a z z'/|z|^2) S')'; restated as the rank-1 Cholesky update
    (a >= 0) / downdate (a < 0) of S with sqrt(|a|/|z|^2) u, u = S z, in the kernels' order
    (mcmc.jl_amd/csrc/ram.hpp ram_update). */
@@ -515,7 +515,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
     const int64_t max_leaps = s->max_leaps > 0 ? s->max_leaps : ((int64_t)1 << 20);
 
     for (int64_t t = 0; t < len; ++t) {
-        const int64_t i = step0 + t + 1;      /* the sampler's loop counter (HMC.jl:252 `for i in 1:Inf`) */
+        const int64_t i = step0 + t + 1;      /* the sampler's loop counter (HMC.jl:126 `for i in 1:Inf`) */
         int acc = 0;
         double ram_ratio = 0.0, ram_nz = 0.0;
         double p_da = 0.0;
@@ -531,7 +531,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 lp = lpp;
             }
         } else if (s->kind == ORC_RAM) {
-            /* RAM.jl:58-81 */
+            /* RAM.jl:58-78 */
             double* Lc = st->ram_L + c;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* rvec = randn(d) */
             double nz = 0.0;
@@ -581,7 +581,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 if (tuned) n_acc += 1;
             }
         } else {
-            /* HMC.jl:252-299 / HMCDA.jl:97-142 */
+            /* HMC.jl:126-173 / HMCDA.jl:97-142 */
             const int da = s->kind == ORC_HMCDA;
             if (!da && tuned) n_prop += 1;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* state0.m = randn(model.size) */
@@ -633,7 +633,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
                 for (int j = 0; j < d; ++j) grads[((size_t)kk * d + j) * C + c] = g[j];
             if (acc_out) acc_out[(size_t)kk * C + c] = (uint8_t)acc;
         }
-        /* adaptation, with the runner's burnin (`i <= runner.burnin`, MALA.jl:116, HMC.jl:293) */
+        /* adaptation, with the runner's burnin (`i <= runner.burnin`, MALA.jl:116, HMC.jl:167) */
         if (s->kind == ORC_RAM) {
             orc_ram_update(st->ram_L + c, C, d, i, ram_ratio, s->rate, ram_nz, gp);
         } else if (s->kind == ORC_MALA && tuned && i <= burnin && (i % s->adapt_step) == 0) {

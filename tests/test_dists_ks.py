@@ -19,9 +19,14 @@ evidence; what carries over is the criterion.  Each case is checked two ways:
   D = KS / sqrt(n) falls with the run length (0.039 at 10^4 steps, 0.031 at 10^5, 0.027 at 4 10^5; checked by
   test_mala_lognormal_converges).  The reference threshold (KS < 10) holds for every case.
 
-CPU: on the oracle (oracle/oracle.c).  GPU (`-m gpu`): the same cases on the HIP kernels with 1 024 chains
-for the pooled bound (every 100th kept sample of every 2nd chain), and the oracle's single chain reproduced
-bit for bit by the HIP path's chain 0.  scipy.stats supplies the exact cdfs (Distributions.jl's
+CPU: on the oracle (oracle/oracle.c).  GPU (`-m gpu`): the same cases on the HIP kernels with 1 024 chains,
+and the oracle's single chain reproduced bit for bit by the HIP path's chain 0.  With 1 024 chains the
+within-chain pooling above is too correlated to carry a 0.1 % bound (at 512 chains x 91 draws, MALA on
+Beta(3, 2), HMC on Cauchy(0, 1) and MALA on LogNormal(-1, 1) reach 2.2, 3.1 and 7.2 on the oracle: chains that
+sit in a tail for thousands of steps), so the GPU bound is taken across chains instead: the 1 024 chains are
+independent, so their kept samples at one step are 1 024 independent draws, and their KS measure follows the
+Kolmogorov distribution once the chains have converged.  It is checked at kept rows 4 500 and 9 000 (the
+largest of the 114 values is 1.55, LogNormal(-1, 1) MALA, on the oracle).  scipy.stats supplies the exact cdfs (Distributions.jl's
 parameterisations: Weibull(shape, scale), Gamma(shape, scale), Exponential(scale), Laplace(mu, scale)).
 """
 import math
@@ -143,9 +148,9 @@ def test_ks_hip(gpu, name, params, dist, which):
     assert np.array_equal(chain.diagnostics["accept"][0], a1[:, 0].astype(bool))
     ksv1 = ks_value(s[:, 0, 0], dist)
     assert ksv1 < KSTHRESHOLD
-    ksv = ks_value(s[::100, 0, ::2], dist)                                  # 91 x 512 pooled draws
-    bound = pooled_bound(name, params, which)
-    assert ksv < bound, f"{which} on {name}{params}: pooled KS {ksv:.3f} > {bound}"
+    for row in (4500, 9000):                                                # 1 024 independent draws each
+        ksv = ks_value(s[row, 0, :], dist)
+        assert ksv < KS_CRIT_001, f"{which} on {name}{params}: KS across chains at kept row {row}: {ksv:.3f}"
 
 
 @pytest.mark.gpu

@@ -19,7 +19,7 @@ def test_ram_constructors_and_asserts():
     for r in (0.0, 1.0, -0.1, 1.5):
         with pytest.raises(AssertionError, match=r"target acceptance rate \(.*\) should be between 0 and 1"):
             mc.RAM(1.0, r)
-    assert not mc.RAM().uses_gradient                  # RAM needs only model.eval (RAM.jl:46-62)
+    assert not mc.RAM().uses_gradient                  # RAM needs only model.eval (RAM.jl:52,61)
 
 
 def _normals(chain, step, d):
@@ -36,7 +36,7 @@ def _accept_u(chain, step):
 
 
 def _ram_literal(m, sampler, chain, steps):
-    """RAM.jl:48-82 transcribed literally in numpy: proposal pars + S*rvec, ratio > 0 || ratio > log(rand()),
+    """RAM.jl:50-78 transcribed literally in numpy: proposal pars + S*rvec, ratio > 0 || ratio > log(rand()),
     eta = min(1, d*i^(-2/3)), SS = S*(I + rvec*rvec'/dot(rvec,rvec)*eta*(min(1,exp(ratio))-rate))*S',
     S = chol(SS)'.  LAPACK's Cholesky replaces Julia's chol: agreement is to rounding, not bitwise."""
     d = m.size
