@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "mcmc.jl_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F64_MFMA_PEAK_TFS = 78.6       # MI355X spec, dense fp64 matrix (not in the guide; measured in DESIGN.md §7)
+VALU_PEAK_TCYC = 1024 * 2.4e9 / 1e12   # VALU issue: 256 CUs x 4 SIMDs, one instruction-cycle each, at 2.4 GHz
 
 # BASELINE.json configs.  chains are per GPU; steps/warmup are the defaults when not given.
 CONFIGS = {
@@ -124,35 +125,38 @@ def hbm_bytes_per_unit(d, sampler):
     return per_step, per_kept
 
 
-def kernel_name(cfg, d, sampler):
-    if cfg["model"] != "iso":
-        if sampler == "mala" and d <= 128:
-            return f"glm_mala1<{next(m for m in (1, 2, 4, 8) if 16 * m >= d)}>"
-        nm = 1
-        while d <= 128 and 16 * nm < d:
-            nm *= 2
-        nw = 1 if d <= 128 else next(w for w in (4, 8) if 64 * w >= d)
-        nm = nm if d <= 128 else 4
-        return f"glm_{'hmc' if sampler.startswith('hmc') else sampler}<{nm},{nw}{',DA' if sampler == 'hmcda' else ''}>"
-    return f"{'lpc' if d <= 32 else 'wpc'}_{sampler}"
+def _norm_kernel(name):
+    """'void mcmc::lpc_rwm<8, true, mcmc::IsoDot, true>(mcmc::KernelArgs)' -> 'lpc_rwm<8,true,IsoDot,true>'."""
+    n = name.split("(")[0].replace("void ", "").replace("mcmc::", "").replace(" ", "")
+    return n
 
 
 def measured_traffic(wkey, kname):
     """HBM bytes per launch of the step kernel for this workload: 2 x FETCH_SIZE + WRITE_SIZE of the timed
     dispatch(es) in a committed rocprofv3 run of the same bench command (MI355X_MICROARCH.md §HBM correction),
-    or None when no profile of this exact workload and this kernel is committed (a profile of an earlier
+    or None when no profile of this exact workload and this kernel instance is committed (a profile of another
     kernel for the same workload is stale and is not used)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
     e = json.load(open(p)).get(wkey)
-    if e is None:
-        return None
-    want = "mcmc::" + kname.replace(",DA", ",true").rstrip(">")     # e.g. mcmc::glm_hmc<4,8,true
-    if want not in e["kernel"].replace(" ", ""):
+    if e is None or _norm_kernel(e["kernel"]) != _norm_kernel(kname):
         return None
     return {"bytes_per_launch": e["traffic_bytes"], "read_bytes": e["read_bytes"], "write_bytes": e["write_bytes"],
             "source": e["source"], "unit": "B"}
+
+
+def measured_valu(kname):
+    """VALU issue cost of the step kernel per chain-step (SQ_ACTIVE_INST_VALU quad-cycles / chain-steps of the
+    timed dispatch) and its measured VALU-busy fraction, from a committed rocprofv3 PMC run of this kernel
+    instance (profiles/valu.json, written by scripts/summarize_valu.py), or None."""
+    p = os.path.join(ROOT, "profiles", "valu.json")
+    if not os.path.exists(p):
+        return None
+    for k, e in json.load(open(p)).items():
+        if _norm_kernel(k) == _norm_kernel(kname):
+            return e
+    return None
 
 
 def host_cpus():
@@ -398,32 +402,59 @@ def main():
     # per-GPU workload key: the PMC traffic of a committed rocprofv3 run of this same workload
     # (profiles/traffic.json, written by scripts/summarize_prof.py) fills roofline.traffic
     wkey = f"{args.config}|d={d}|chains={C}|{args.sampler}|steps={K}|thinning={args.thinning}|spl={spl}"
-    kname = kernel_name(cfg0, d, args.sampler)
+    kname = task.step_kernel                            # the instance the timed run launched (C ABI)
     tdet = measured_traffic(wkey, kname)
     traffic = tdet["bytes_per_launch"] if tdet else None
     avg_launch_s = kernel_ms * 1e-3 / launches          # HIP events around the launches, on their stream
+    units = C * K / launches                            # chain-steps per launch
     if cfg0["model"] == "iso":
+        # HBM: the fused kernel reads and writes the chain state once per launch (x [d][C], lp [C]) and
+        # streams the kept samples (+ gradients) and accept bits; SURVEY.md §8(d)'s per-step state round trip
+        # (16 d + 16 + 1/8 B per chain-step) is what an unfused step would move, kept as `survey_bytes`
         per_step, per_kept = hbm_bytes_per_unit(d, args.sampler)
-        nbytes = C * K * per_step + C * nkept * per_kept               # per run = per launch x launches
-        achieved = nbytes / launches / avg_launch_s / 1e9
-        moved = (launches * C * (16 * d + 16) + C * nkept * per_kept) / launches / avg_launch_s / 1e9
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname, "launches": launches,
-                "avg_launch_ms": avg_launch_s * 1e3,
-                "algorithmic_bytes_per_launch": nbytes / launches,
-                "units_per_launch": C * K / launches,
-                "bytes_per_unit": {"chain_step": per_step, "kept_chain_step": per_kept},
-                "state_resident_GBps": moved,
-                "note": "units = chain-steps; the fused kernel keeps chain state in VGPRs across the launch's "
-                        "steps, so HBM moves state once per launch (state_resident_GBps) and the kernel is "
-                        "fp64-VALU bound (DESIGN.md §5)"}
+        state_b = 2 * C * (8 * d + 8)                  # x [d][C] and lp [C], read and written
+        fused = launches * state_b + C * nkept * (per_kept + 1 / 8)
+        hbm_ach = fused / launches / avg_launch_s / 1e9
+        survey = C * K * per_step + C * nkept * per_kept
+        hbm = {"achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
+               "algorithmic_bytes_per_launch": fused / launches, "traffic": traffic, "traffic_detail": tdet,
+               "note": "fused design: chain state in and out once per launch + kept samples/gradients + accept bits"}
+        survey_bytes = {"bytes_per_unit": {"chain_step": per_step, "kept_chain_step": per_kept},
+                        "equivalent_GBps": survey / launches / avg_launch_s / 1e9,
+                        "note": "SURVEY.md §8(d) bytes of an unfused step (state round trip every step); the "
+                                "fused kernel never moves them, so this rate can exceed HBM peak: it is the north "
+                                "star's '% of HBM roofline' yardstick, not a roofline"}
+        vm = measured_valu(kname)
+        if vm is not None:
+            # the binding resource: VALU issue.  SQ_ACTIVE_INST_VALU quad-cycles x 4 = SIMD-cycles of VALU issue
+            # per chain-step (measured, committed profile of this kernel instance); achieved = that x chain-steps
+            # per launch / the live launch time; peak = 1024 SIMDs x 2.4 GHz (the spec engine clock)
+            cyc = 4.0 * vm["valu_quadcycles_per_chain_step"]
+            ach = cyc * units / avg_launch_s / 1e12
+            roof = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TCYC, "unit": "T VALU-issue-cycles/s",
+                    "frac": ach / VALU_PEAK_TCYC, "traffic": traffic, "kernel": kname, "launches": launches,
+                    "avg_launch_ms": avg_launch_s * 1e3, "units_per_launch": units,
+                    "valu_cycles_per_unit": cyc, "valu_busy_measured": vm["valu_busy"],
+                    "clock_ghz_measured": vm["clock_ghz"], "valu_source": vm["source"],
+                    "hbm": hbm, "survey_bytes": survey_bytes,
+                    "note": "units = chain-steps; VALU cycles per unit from rocprofv3 PMC (SQ_ACTIVE_INST_VALU); "
+                            "valu_busy_measured = SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES of that profile (at "
+                            "the measured clock); HBM moves only the per-launch state and the kept outputs "
+                            "(hbm.frac)"}
+        else:
+            roof = {"bound": "hbm", "achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm_ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname,
+                    "launches": launches, "avg_launch_ms": avg_launch_s * 1e3,
+                    "algorithmic_bytes_per_launch": fused / launches, "units_per_launch": units,
+                    "survey_bytes": survey_bytes,
+                    "note": "no committed VALU profile of this kernel instance: HBM roofline of the fused design"}
     else:
         flop_per_eval = 4.0 * cfg0["n"] * d                           # eta = X beta, then X^T r
         flops = flop_per_eval * evals
         achieved = flops / launches / avg_launch_s / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname, "launches": launches,
-                "avg_launch_ms": avg_launch_s * 1e3, "flop_per_eval": flop_per_eval,
+                "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname,
+                "launches": launches, "avg_launch_ms": avg_launch_s * 1e3, "flop_per_eval": flop_per_eval,
                 "evals_per_launch": evals / launches,
                 "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
                         "device); 4 n d fp64 flop each (SURVEY.md §8(d))"}

@@ -32,7 +32,9 @@
  * @assert texts are reproduced verbatim where one exists.
  *
  * Threading: one host thread drives a context; calls on one context are not
- * re-entrant; distinct contexts are independent.  Ownership: the caller owns
+ * re-entrant; distinct contexts are independent and may be driven from
+ * different host threads at once (also on one GPU).  mcmc_group_* drives
+ * several GPUs from one host thread (library worker threads per device).  Ownership: the caller owns
  * every output buffer; the library owns device state inside ctx/model/chains
  * and never keeps a caller pointer after a call returns.
  */
@@ -214,6 +216,45 @@ int mcmc_chains_store_leaps(mcmc_chains* chains, int64_t cap, double* pars, doub
 
 /* run_serialmc: consume runner->len steps, keep (burnin+1):thinning:len. */
 int mcmc_run_serialmc(mcmc_chains* chains, const mcmc_runner_cfg* runner, mcmc_outputs* out);
+
+/* ---- one node's GPUs driven by one host thread (SURVEY.md §8(b),(e)) ----
+ * Replaces the reference's only parallel path, prun -> pmap of independent tasks over worker processes
+ * (src/runners/runners.jl:35-42, examples/parallel_serialmc.jl:1-8): one batch of nchains chains is split
+ * into contiguous blocks of whole 64-chain groups, block g on devices[g] (mcmc_group_plan).  Every block
+ * keys its random streams by global chain id (chain_offset + its first chain), so the results are
+ * bit-identical to one context running all chains, for any device list.  A run launches every block's step
+ * loop concurrently (one library worker thread per block, each with its own context and stream; no
+ * collective inside the step loop), then gathers each block's outputs device -> host straight into the
+ * caller's [nkept][d][nchains] buffers (a strided copy per GPU over that GPU's own host link: the end
+ * gather of MCMCChain assembly, timed apart).  A device may be listed more than once (several blocks on one
+ * GPU).  Outputs of a group run are host buffers (on_device must be 0). */
+typedef struct mcmc_group mcmc_group;
+typedef struct mcmc_group_chains mcmc_group_chains;
+int mcmc_group_create(const int32_t* devices, int32_t ndevices, mcmc_group** out);
+int mcmc_group_destroy(mcmc_group* group);     /* after every mcmc_group_chains of it is destroyed */
+int mcmc_group_size(mcmc_group* group, int32_t* ndevices);
+/* the block of every device: block g = chains [first[g], first[g] + count[g]); blocks of ceil(nchains /
+ * nblocks) rounded up to a multiple of 64 chains, so trailing blocks may be short or empty (count 0).
+ * Host-only arithmetic (no device needed). */
+int mcmc_group_plan(int64_t nchains, int32_t nblocks, int64_t* first, int64_t* count);
+/* model (replicated: uploaded once per device), sampler and chains on every device; init_x: optional
+ * [d][nchains] host array (NULL -> model.init) */
+int mcmc_group_chains_create(mcmc_group* group, const mcmc_model_desc* model, const mcmc_sampler_cfg* sampler,
+                             int64_t nchains, int64_t chain_offset, uint64_t seed, const double* init_x,
+                             mcmc_group_chains** out);
+int mcmc_group_chains_destroy(mcmc_group_chains* gc);
+int mcmc_group_chains_reset(mcmc_group_chains* gc);                       /* resume(): every block */
+int mcmc_group_chains_steps_done(mcmc_group_chains* gc, int64_t* steps);
+int mcmc_group_chains_set_steps_per_launch(mcmc_group_chains* gc, int64_t steps_per_launch);
+/* block g's chains (NULL when the block is empty) and its first chain / chain count; the block's
+ * mcmc_chains may be queried (evals, step kernel, RAM factor) but not run or destroyed on its own */
+int mcmc_group_chains_block(mcmc_group_chains* gc, int32_t g, mcmc_chains** chains, int64_t* first,
+                            int64_t* count);
+/* run_serialmc on every block concurrently; out holds host buffers for all nchains chains (mcmc_outputs
+ * layout); out->runtime_s / kernel_ms: the slowest block's step loop; gather_s (may be NULL): the slowest
+ * block's device -> host gather of its outputs. */
+int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_cfg* runner, mcmc_outputs* out,
+                            double* gather_s);
 
 /* ---- SeqMC population runner (src/runners/SeqMC.jl:21-122) ----
  * targets[t] (t < ntargets) are chain batches of one context, equal d, each with nchains == npart:

@@ -16,6 +16,7 @@
 
 #include "../../../include/mcmc_hip.h"
 #include "../common.hpp"
+#include "internal.hpp"
 #include "kernels_api.hpp"
 
 using namespace mcmc;
@@ -38,6 +39,7 @@ static int fail(int code, const std::string& msg) {
     } while (0)
 
 extern "C" const char* mcmc_last_error(void) { return g_err.c_str(); }
+int mcmc_set_error(int code, const std::string& msg) { return fail(code, msg); }
 
 // the step kernel instance the last launch function on this thread dispatched (kernels_api.hpp)
 #include <cstdarg>
@@ -824,8 +826,29 @@ extern "C" int mcmc_chains_store_leaps(mcmc_chains* c, int64_t cap, double* pars
 }
 
 // ------------------------------------------------------------------ run
+// device -> host copy of `rows` rows of `width` bytes from a packed device array into a host array whose
+// rows are `dpitch` bytes apart (dpitch == width: one contiguous copy)
+static hipError_t d2h_rows(mcmc_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t width, size_t rows) {
+    hipError_t e = dpitch == width
+                       ? hipMemcpyAsync(dst, src, width * rows, hipMemcpyDeviceToHost, ctx->stream)
+                       : hipMemcpy2DAsync(dst, dpitch, src, width, width, rows, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e;
+}
+
 extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs* out) {
+    return mcmc_run_serialmc_ld(c, r, out, c ? c->C : 0, nullptr);
+}
+
+// run_serialmc with host outputs laid out for a larger chain batch this one is a block of (mcmc_group.cpp):
+// samples/gradients/final_x rows are ldc chains apart, accept-bit rows ceil(ldc/64) words apart; the caller
+// has offset every pointer to this block's first chain (a multiple of 64 when ldc != C).  copy_s: the
+// device -> host time of the outputs.
+int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs* out, int64_t ldc, double* copy_s) {
     if (!c || !r) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    if (ldc < c->C) return fail(MCMC_E_INVALID_ARG, "output leading dimension below the chain count");
+    if (out && out->on_device && ldc != c->C)
+        return fail(MCMC_E_INVALID_ARG, "strided outputs are host buffers");
     if (int rc = mcmc_runner_validate(r)) return rc;
     mcmc_model* m = c->model;
     mcmc_ctx* ctx = m->ctx;
@@ -967,10 +990,13 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
         out->nkept = nkept;
         out->runtime_s = std::chrono::duration<double>(t1 - t0).count();
         out->kernel_ms = ms;
+        const size_t rowb = (size_t)C * 8, drow = (size_t)ldc * 8;
+        const size_t nwl = (size_t)(ldc + 63) / 64;
+        auto c0 = std::chrono::steady_clock::now();
         if (!on_dev) {
-            if (want_samples) HIP_TRY(d2h(ctx, out->samples, d_samples, nsamp * 8));
-            if (want_grads) HIP_TRY(d2h(ctx, out->gradients, d_grads, nsamp * 8));
-            if (want_bits) HIP_TRY(d2h(ctx, out->accept_bits, d_bits, (size_t)nkept * nw * 8));
+            if (want_samples) HIP_TRY(d2h_rows(ctx, out->samples, drow, d_samples, rowb, (size_t)nkept * d));
+            if (want_grads) HIP_TRY(d2h_rows(ctx, out->gradients, drow, d_grads, rowb, (size_t)nkept * d));
+            if (want_bits) HIP_TRY(d2h_rows(ctx, out->accept_bits, nwl * 8, d_bits, (size_t)nw * 8, (size_t)nkept));
         }
         if (out->final_x) {
             if (on_dev) {
@@ -978,13 +1004,14 @@ extern "C" int mcmc_run_serialmc(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_
             } else {
                 if (int rc = ensure(c->out_tmp, (size_t)d * C * 8)) return rc;
                 HIP_TRY(state_to_cols(L, (double*)c->out_tmp.p, C, c->st.x, c->ld, d, C, st));
-                HIP_TRY(hipMemcpyAsync(out->final_x, c->out_tmp.p, (size_t)d * C * 8, hipMemcpyDeviceToHost, st));
+                HIP_TRY(d2h_rows(ctx, out->final_x, drow, c->out_tmp.p, rowb, (size_t)d));
             }
         }
         if (out->final_lp)
             HIP_TRY(hipMemcpyAsync(out->final_lp, c->st.lp, (size_t)C * 8,
                                    on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        if (copy_s) *copy_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
     }
     return MCMC_OK;
 }

@@ -154,6 +154,14 @@ class MCMCLikelihoodModel:
     def _handle(self, device: int) -> ct.c_void_p:
         if device in self._dev:
             return self._dev[device]
+        desc = self._desc()
+        h = ct.c_void_p()
+        check(_lib.load().mcmc_model_create(_ctx(device), ct.byref(desc), ct.byref(h)))
+        self._dev[device] = h
+        return h
+
+    def _desc(self) -> _lib.ModelDesc:
+        """The C ABI model descriptor (its pointers borrow this model's arrays)."""
         t = self.target
         desc = _lib.ModelDesc()
         desc.kind = t.kind
@@ -171,10 +179,7 @@ class MCMCLikelihoodModel:
             desc.n = t.X.shape[0]
             desc.X = dptr(t.X)
             desc.Y = dptr(t.Y)
-        h = ct.c_void_p()
-        check(_lib.load().mcmc_model_create(_ctx(device), ct.byref(desc), ct.byref(h)))
-        self._dev[device] = h
-        return h
+        return desc
 
     def eval(self, x, device: int = 0):
         """model.eval on a batch: x [d] or [d, nchains] -> lp (likmodel.jl:21)."""
@@ -452,8 +457,10 @@ class MCMCTask:
     """A batch of `nchains` independent chains of (model, sampler, runner) on one GPU (MCMC.jl:33-39)."""
 
     def __init__(self, model: MCMCLikelihoodModel, sampler: _Sampler, runner: SerialMC, nchains: int = 1,
-                 seed: int = 1, device: int = 0, chain_offset: int = 0, init_x=None, steps_per_launch: int = 0):
+                 seed: int = 1, device: int = 0, chain_offset: int = 0, init_x=None, steps_per_launch: int = 0,
+                 devices: Optional[Sequence[int]] = None):
         self._h = None
+        self._group = None
         if not isinstance(runner, SerialMC) and type(runner).__name__ != "SeqMC":
             raise NotImplementedError("runners: SerialMC (one batch) or SeqMC (lists of targets, run_seqmc)")
         if sampler.uses_gradient and not model.has_gradient:
@@ -465,15 +472,37 @@ class MCMCTask:
         self.init_x = None if init_x is None else np.ascontiguousarray(
             np.asarray(init_x, dtype=np.float64).reshape(model.size, self.nchains))
         self.steps_per_launch = int(steps_per_launch)
+        # devices: run the batch as one mcmc_group over these GPUs (contiguous 64-chain-aligned blocks, one
+        # per listed device; a device may repeat); None: one context on `device`
+        self.devices = None if devices is None else tuple(int(x) for x in devices)
+        if self.devices is not None and len(self.devices) == 0:
+            raise ValueError("devices must list at least one GPU")
 
     def batch(self, nchains: int, seed: Optional[int] = None, **kw) -> "MCMCTask":
         """Same (model, sampler, runner) over `nchains` chains."""
         return MCMCTask(self.model, self.sampler, self.runner, nchains=nchains,
                         seed=self.seed if seed is None else seed, device=kw.get("device", self.device),
                         chain_offset=kw.get("chain_offset", self.chain_offset), init_x=kw.get("init_x"),
-                        steps_per_launch=kw.get("steps_per_launch", self.steps_per_launch))
+                        steps_per_launch=kw.get("steps_per_launch", self.steps_per_launch),
+                        devices=kw.get("devices", self.devices))
 
     def handle(self) -> ct.c_void_p:
+        """The mcmc_chains (one context) or, with `devices`, the mcmc_group_chains of this task."""
+        if self._h is None and self.devices is not None:
+            lib = _lib.load()
+            g = ct.c_void_p()
+            devs = (ct.c_int32 * len(self.devices))(*self.devices)
+            check(lib.mcmc_group_create(devs, len(self.devices), ct.byref(g)))
+            self._group = g
+            h = ct.c_void_p()
+            desc = self.model._desc()
+            cfg = self.sampler.cfg()
+            check(lib.mcmc_group_chains_create(g, ct.byref(desc), ct.byref(cfg), self.nchains, self.chain_offset,
+                                               ct.c_uint64(self.seed & 0xFFFFFFFFFFFFFFFF), dptr(self.init_x),
+                                               ct.byref(h)))
+            if self.steps_per_launch:
+                check(lib.mcmc_group_chains_set_steps_per_launch(h, self.steps_per_launch))
+            self._h = h
         if self._h is None:
             mh = self.model._handle(self.device)
             h = ct.c_void_p()
@@ -486,12 +515,28 @@ class MCMCTask:
             self._h = h
         return self._h
 
+    def blocks(self):
+        """[(mcmc_chains handle or None, first chain, chain count)] per listed device (group tasks), or the
+        single batch as one block."""
+        h = self.handle()
+        if self.devices is None:
+            return [(h, 0, self.nchains)]
+        out = []
+        for b in range(len(self.devices)):
+            c, f, n = ct.c_void_p(), ct.c_int64(), ct.c_int64()
+            check(_lib.load().mcmc_group_chains_block(h, b, ct.byref(c), ct.byref(f), ct.byref(n)))
+            out.append((c if c.value else None, f.value, n.value))
+        return out
+
     @property
     def steps_done(self) -> int:
         if self._h is None:
             return 0
         v = ct.c_int64(0)
-        check(_lib.load().mcmc_chains_steps_done(self._h, ct.byref(v)))
+        if self.devices is not None:
+            check(_lib.load().mcmc_group_chains_steps_done(self._h, ct.byref(v)))
+        else:
+            check(_lib.load().mcmc_chains_steps_done(self._h, ct.byref(v)))
         return v.value
 
     @property
@@ -499,16 +544,20 @@ class MCMCTask:
         """Log-target evaluations over all chains since the chains were created/reset."""
         if self._h is None:
             return 0
-        v = ct.c_int64(0)
-        check(_lib.load().mcmc_chains_evals(self._h, ct.byref(v)))
-        return v.value
+        tot = 0
+        for c, _, _ in self.blocks():
+            if c is not None:
+                v = ct.c_int64(0)
+                check(_lib.load().mcmc_chains_evals(c, ct.byref(v)))
+                tot += v.value
+        return tot
 
     @property
     def step_kernel(self) -> str:
         """The step kernel instance the last run launched (mcmc_chains_step_kernel), e.g.
-        "lpc_rwm<8, true, IsoDot, true>"; "" before the first run."""
+        "lpc_rwm<8, true, IsoDot, true>"; "" before the first run (group tasks: block 0's)."""
         buf = ct.create_string_buffer(160)
-        check(_lib.load().mcmc_chains_step_kernel(self.handle(), buf, len(buf)))
+        check(_lib.load().mcmc_chains_step_kernel(self.blocks()[0][0], buf, len(buf)))
         return buf.value.decode()
 
     def ram_factor(self) -> np.ndarray:
@@ -517,19 +566,31 @@ class MCMCTask:
             raise AssertionError("the task has not run")
         d, C = self.model.size, self.nchains
         packed = np.empty((d * (d + 1) // 2, C))
-        check(_lib.load().mcmc_chains_ram_factor(self._h, packed.ctypes.data))
+        for c, f, n in self.blocks():
+            if c is not None:
+                part = np.empty((d * (d + 1) // 2, n))
+                check(_lib.load().mcmc_chains_ram_factor(c, part.ctypes.data))
+                packed[:, f:f + n] = part
         return unpack_ram_factor(packed, d)
 
     def reset(self) -> None:
         if self._h is not None:
-            check(_lib.load().mcmc_chains_reset(self._h))
+            if self.devices is not None:
+                check(_lib.load().mcmc_group_chains_reset(self._h))
+            else:
+                check(_lib.load().mcmc_chains_reset(self._h))
 
     def __del__(self):
-        if getattr(self, "_h", None) is not None:
-            try:
-                _lib.load().mcmc_chains_destroy(self._h)
-            except Exception:
-                pass
+        try:
+            if getattr(self, "_h", None) is not None:
+                if self.devices is not None:
+                    _lib.load().mcmc_group_chains_destroy(self._h)
+                else:
+                    _lib.load().mcmc_chains_destroy(self._h)
+            if getattr(self, "_group", None) is not None:
+                _lib.load().mcmc_group_destroy(self._group)
+        except Exception:
+            pass
 
 
 class MCMCChain:
@@ -606,6 +667,8 @@ def _run_task(t: MCMCTask) -> MCMCChain:
     out.final_lp = flp.ctypes.data
     out.on_device = 0
     leaps = None
+    if t.devices is not None and getattr(t.sampler, "storeLeaps", False):
+        raise NotImplementedError("storeLeaps on a group task: run the batch on one device")
     if getattr(t.sampler, "storeLeaps", False):              # HMC.jl:145-150 / HMCDA.jl:110-117
         cap = t.sampler.leaps_cap()
         leaps = {"pars": np.empty((nk, cap + 1, d, C)), "grad": np.empty((nk, cap + 1, d, C)),
@@ -614,8 +677,16 @@ def _run_task(t: MCMCTask) -> MCMCChain:
         check(lib.mcmc_chains_store_leaps(h, cap, *(leaps[k].ctypes.data for k in
                                                     ("pars", "grad", "m", "logTarget", "H", "nleaps"))))
     cfg = r.cfg()
-    check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
+    gather_s = None
+    if t.devices is not None:
+        gs = ct.c_double(0.0)
+        check(lib.mcmc_group_run_serialmc(h, ct.byref(cfg), ct.byref(out), ct.byref(gs)))
+        gather_s = gs.value
+    else:
+        check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
     diags = {"step": list(r.r), "accept": _unpack_bits(bits, C)}
+    if gather_s is not None:
+        diags["gather_s"] = gather_s                         # end gather of the group run, timed apart
     if leaps is not None:
         # per kept step: the trajectory's states, leap 0 = state0 (the reference's leapStates array of
         # HMCSample(pars, grad, m, logTarget, H)), NaN past nleaps
@@ -651,5 +722,5 @@ def resume(c, steps: int = 100):
     t = c.task if isinstance(c, MCMCChain) else c
     nt = MCMCTask(t.model, t.sampler, SerialMC(steps=steps, thinning=t.runner.thinning), nchains=t.nchains,
                   seed=t.seed, device=t.device, chain_offset=t.chain_offset, init_x=t.init_x,
-                  steps_per_launch=t.steps_per_launch)
+                  steps_per_launch=t.steps_per_launch, devices=t.devices)
     return _run_task(nt)

@@ -814,17 +814,18 @@ void orc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* o
  * (ess.jl:6-10): n * var_iid / var_vtype with var_iid = var(x)/n (var.jl:7-8), and
  * vtype 1 = Geyer IMSE (var.jl:45-75), 2 = IPSE (var.jl:95-117), 3 = batch means (var.jl:20-27).
  * Autocovariances as StatsBase acf(x, lags, correlation=false): sum_t z_t z_{t+k} / n.
- * Sums left to right, multiply then add -- the order kernels/stats.hip uses. */
+ * Sums left to right; sums of products (ss and the lag sums) accumulate with fma(z_t, z_{t+k}, s) -- the
+ * order and rounding kernels/stats.hip uses. */
 static double orc_ess_one(const double* x, size_t stride, int64_t n, int vtype, int64_t maxlag, int64_t bl,
                           double* var_out) {
     const double nd = (double)n;
     double sum = 0.0;
     for (int64_t t = 0; t < n; ++t) sum = sum + x[(size_t)t * stride];
     const double mean = sum / nd;
-    double ss = 0.0;
+    double ss = 0.0;                          /* sums of products accumulate with fma (kernels/stats.hip) */
     for (int64_t t = 0; t < n; ++t) {
         const double z = x[(size_t)t * stride] - mean;
-        ss = ss + z * z;
+        ss = fma(z, z, ss);
     }
     const double var_iid = (ss / (nd - 1.0)) / nd;
     double var_v;
@@ -859,7 +860,7 @@ static double orc_ess_one(const double* x, size_t stride, int64_t n, int vtype, 
                 }
                 double s = 0.0;
                 for (int64_t t = 0; t + lag < n; ++t)
-                    s = s + (x[(size_t)t * stride] - mean) * (x[(size_t)(t + lag) * stride] - mean);
+                    s = fma(x[(size_t)t * stride] - mean, x[(size_t)(t + lag) * stride] - mean, s);
                 acv[h] = s / nd;
             }
             double g = acv[0] + acv[1];

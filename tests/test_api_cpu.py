@@ -177,14 +177,30 @@ def test_store_leaps_options():
 
 def test_bench_traffic_only_from_a_profile_of_the_same_kernel():
     """bench.py fills roofline.traffic from profiles/traffic.json only when the committed profile is of the same
-    workload AND the same step kernel (a profile of an earlier kernel is stale)"""
+    workload AND the same step kernel instance (a profile of another kernel is stale)"""
     import importlib
     import json
     bench = importlib.import_module("bench")
     t = json.load(open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "profiles", "traffic.json")))
     key = next(k for k in t if k.startswith("logistic128|"))
-    assert bench.measured_traffic(key, "glm_mala1<8>")["bytes_per_launch"] == t[key]["traffic_bytes"]
+    assert bench.measured_traffic(key, t[key]["kernel"])["bytes_per_launch"] == t[key]["traffic_bytes"]
     assert bench.measured_traffic(key, "glm_mala<8,1>") is None
     assert bench.measured_traffic("no-such-workload", "lpc_rwm") is None
-    mkey = next(k for k in t if k.startswith("metric|"))
-    assert bench.measured_traffic(mkey, bench.kernel_name(bench.CONFIGS["metric"], 32, "rwm")) is not None
+    # the driver's exact command (bench.py --gpus 1 --steps 20 --warmup 5) has a committed profile
+    dkey = "metric|d=32|chains=1048576|rwm|steps=20|thinning=10|spl=0"
+    assert bench.measured_traffic(dkey, "lpc_rwm<8, true, IsoDot, true>") is not None
+    assert bench.measured_traffic(dkey, "lpc_rwm<8, true, IsoDot, false>") is None
+
+
+def test_bench_valu_roofline_profile():
+    """The metric kernel's VALU roofline inputs come from a committed PMC profile of that kernel instance, and
+    the implied fraction of VALU issue peak is a fraction (<= 1)"""
+    import importlib
+    bench = importlib.import_module("bench")
+    vm = bench.measured_valu("lpc_rwm<8, true, IsoDot, true>")
+    assert vm is not None and os.path.exists(os.path.join(ROOT, vm["source"]))
+    assert 0.0 < vm["valu_busy"] <= 1.0
+    # at the profiled dispatch: cycles per chain-step x chain-steps / duration against 1024 SIMDs x 2.4 GHz
+    units = 1048576 * (20 if "steps=20" in vm["workload_key"] else 1000)
+    frac = 4 * vm["valu_quadcycles_per_chain_step"] * units / vm["duration_s"] / (bench.VALU_PEAK_TCYC * 1e12)
+    assert 0.3 < frac <= 1.0
