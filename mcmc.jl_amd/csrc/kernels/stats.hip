@@ -1,15 +1,16 @@
 // stats.hip -- output analysis on the device: effective sample size of every (chain, parameter)
 // series of a batched MCMCChain (src/stats/ess.jl:6-10, var.jl:7-8,20-27,45-117).
 //
-// The C-ABI sample layout [nkept][d][C] makes 64 consecutive chains of one parameter one coalesced
-// 512 B row per kept step t.  k_ess_tile (n up to kEssTileMaxN): a 256-thread block stages the n x 64 tile
-// of its 64 series in LDS once; one lane per series sums and centres its series in place (z_t = x_t - mean);
-// then four lanes per series compute Geyer's lag pairs four at a time (lane q of round r: the pair
-// j = 4r + q, lags 2j and 2j + 1), share the four pair sums, and every lane of the group runs the
-// sequential initial-sequence scan on them; the rounds stop at the series' first non-positive pair
-// (at most three pairs are computed past it and discarded).  The lag sums read LDS only (no HBM re-reads):
-// one read of z_t (broadcast to the group) and one of z_{t+2j+1} per step, two FMAs.  Longer series
-// (k_ess_col) keep one thread per series and re-read the column from global memory (L2) per lag.
+// The C-ABI sample layout [nkept][d][C] makes consecutive chains of one parameter one coalesced row per kept
+// step t.  k_ess_tile (n up to kEssTileMaxN): a 128-thread block stages the n x 32 tile of its 32 series in LDS
+// once, series-major (plus a zero pad); one lane per series sums and centres its series in place (z_t = x_t - mean);
+// then four lanes per series compute Geyer's lag pairs, first one pair per lane (pairs 0-3: a series of nearly
+// independent draws stops there), then four consecutive pairs (eight lags) per lane per round, sixteen pairs
+// per series and round.  A lane keeps its eight shifted values in a register window, so each step of its lag
+// sums costs one ds_read_b128 per two steps and eight FMAs per step.  The group shares the pair sums and every lane of it runs the
+// sequential initial-sequence scan on them; pairs computed past the series' first non-positive pair are
+// discarded.  No HBM re-reads.  Longer series (k_ess_col) keep one thread per series and re-read the column
+// from global memory (L2) per lag.
 //
 // Arithmetic order (restated bit for bit by oracle/oracle.c orc_ess): the sum of x and every lag sum
 // left to right over t; ss and the autocovariance sums accumulate with fma(z_t, z_{t+lag}, s); batch sums
@@ -20,11 +21,18 @@
 namespace mcmc {
 
 constexpr int kEssBlock = 64;          // k_ess_col: one thread per series
-constexpr int kEssTile = 64;           // k_ess_tile: series per block
-constexpr int kEssThreads = 256;       // k_ess_tile: 4 lanes per series
-constexpr int kEssRow = 72;            // LDS row stride in doubles: the 4 lag rows of a lane group (2 rows
-                                       // apart) land 32 banks apart, so a wave's 64 reads take the minimum 2 passes
-constexpr int kEssTileMaxN = (160 * 1024) / (kEssRow * 8);    // 284: the tile fits the 160 KB of LDS
+constexpr int kEssTile = 32;           // k_ess_tile: series per block
+constexpr int kEssThreads = 128;       // k_ess_tile: 4 lanes per series
+// k_ess_tile's LDS tile is series-major, [32][S] doubles: a series is contiguous in t, so two consecutive steps
+// come in one ds_read_b128.  S >= n + 16 (a zero pad: the lag loops run in whole 8-step blocks and read up to 15
+// past the series' end) and S = 2 mod 8: the 16 lanes of a ds_read_b128 lane group (4 series x 4 lanes whose
+// windows sit 8 steps apart) then cover the 64 banks once.
+__host__ __device__ constexpr int ess_stride(int n) { return n + 16 + (((2 - (n + 16)) % 8) + 8) % 8; }
+constexpr int kEssTileMaxN = 618;      // 32 x ess_stride(618) x 8 B = 162 304 B: fits the 160 KB of LDS
+static_assert(32 * ess_stride(kEssTileMaxN) * 8 <= 160 * 1024 && 32 * ess_stride(kEssTileMaxN + 1) * 8 > 160 * 1024,
+              "kEssTileMaxN is the largest series the LDS tile holds");
+
+typedef double ess_f64x2 __attribute__((ext_vector_type(2)));
 
 struct EssArgs {
     const double* s;
@@ -67,42 +75,130 @@ __device__ __forceinline__ bool geyer_take(double g, int64_t j, int32_t vtype, d
     return true;
 }
 
+// acc[i] = sum over t < tn (tn a multiple of LPL) of z_t z_{t+L0+i}, in t order: lag L0+i's autocovariance sum
+// once the zero pad has absorbed the terms past the series' end (fma(z, 0, s) = s; s is never -0).  The LPL
+// values z_{t+L0} .. z_{t+L0+LPL-1} ride in a register window rotated by renaming; every two steps take one
+// ds_read_b128 of (z_t, z_{t+1}) (shared by the lane group) and one of the window's next two entries.
+template <int LPL>
+__device__ __forceinline__ void ess_lag_sums(const double* zc, int L0, int tn, double (&acc)[LPL]) {
+    double w[LPL];
+#pragma unroll
+    for (int i = 0; i < LPL; i += 2) {
+        const ess_f64x2 v = *reinterpret_cast<const ess_f64x2*>(zc + L0 + i);
+        w[i] = v.x;
+        w[i + 1] = v.y;
+    }
+#pragma unroll
+    for (int i = 0; i < LPL; ++i) acc[i] = 0.0;
+    for (int t = 0; t < tn; t += LPL) {
+#pragma unroll
+        for (int u = 0; u < LPL; u += 2) {
+            const ess_f64x2 zz = *reinterpret_cast<const ess_f64x2*>(zc + t + u);            // z_{t+u}, z_{t+u+1}
+            const ess_f64x2 nw = *reinterpret_cast<const ess_f64x2*>(zc + t + u + L0 + LPL); // next window pair
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) acc[i] = __builtin_fma(zz.x, w[(i + u) % LPL], acc[i]);
+            w[u] = nw.x;                                                                     // z_{t+u+L0+LPL}
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) acc[i] = __builtin_fma(zz.y, w[(i + u + 1) % LPL], acc[i]);
+            w[u + 1] = nw.y;
+        }
+    }
+}
+
+// one Geyer round: lane q of the group computes pairs p0 + q LPL/2 ... (lags 2 p0 + q LPL ...), the group's
+// 4 LPL/2 pair sums are shared and scanned in pair order by every lane of the group
+template <int LPL>
+__device__ __forceinline__ void ess_round(const double* zc, int n, double nd, int64_t p0, int q, int gl, int64_t k,
+                                          int32_t vtype, bool& done, double& prev, double& gsum) {
+    constexpr int PP = LPL / 2;                                // pairs per lane
+    double g[PP];
+#pragma unroll
+    for (int i = 0; i < PP; ++i) g[i] = 0.0;
+    const int64_t L0 = 2 * (p0 + (int64_t)q * PP);
+    if (!done && p0 + (int64_t)q * PP <= k && L0 < n) {
+        double acc[LPL];
+        const int tn = (int)((n - L0 + LPL - 1) / LPL) * LPL;
+        ess_lag_sums<LPL>(zc, (int)L0, tn, acc);
+#pragma unroll
+        for (int i = 0; i < PP; ++i) g[i] = acc[2 * i] / nd + acc[2 * i + 1] / nd;   // acv[2j] + acv[2j+1]
+    }
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int i = 0; i < PP; ++i) {
+            const double gi = __shfl(g[i], gl + qq, 64);
+            const int64_t jp = p0 + qq * PP + i;
+            if (!done) done = jp > k || !geyer_take(gi, jp, vtype, prev, gsum);
+        }
+}
+
 __global__ __launch_bounds__(kEssThreads) void k_ess_tile(EssArgs a) {
-    extern __shared__ double tile[];                           // [n][kEssRow]: x, then z = x - mean
+    extern __shared__ __attribute__((aligned(16))) double tile[];   // [32][S]: x, then z = x - mean, zero pad
     const int tid = (int)threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * kEssTile;
     const int64_t j = blockIdx.y;
-    const int64_t n = a.n;
+    const int n = (int)a.n;
+    const int S = ess_stride(n);
     const size_t stride = (size_t)a.d * (size_t)a.C;
     const double* base = a.s + (size_t)j * (size_t)a.C;
-    // stage: 4 rows per pass of the block, 8 passes in flight
+    // stage: rows of 32 chains (256 B) from HBM, 4 rows per pass of the block, transposed into the series-major
+    // tile; then the zero pad
     {
-        const int cc = tid & 63;
+        const int cc = tid & 31;
         const bool live = c0 + cc < a.C;
         const double* col = base + (size_t)(live ? c0 + cc : 0);
-        int64_t t = tid >> 6;
-        for (; t + 28 < n; t += 32) {
-            double v[8];
+        double* dst = tile + cc * S;
+        // every row of a 96-row pass requested before the first is written to LDS (24 loads in flight per thread:
+        // the staging is latency-bound otherwise, a block's whole tile being one HBM round trip)
+        for (int t0 = tid >> 5; t0 < n; t0 += 96) {
+            double v[24];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = col[(size_t)(t + 4 * u) * stride];
+            for (int u = 0; u < 24; ++u) {
+                const int t = t0 + 4 * u;
+                v[u] = (live && t < n) ? col[(size_t)t * stride] : 0.0;
+            }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) tile[(size_t)(t + 4 * u) * kEssRow + cc] = live ? v[u] : 0.0;
+            for (int u = 0; u < 24; ++u)
+                if (t0 + 4 * u < n) dst[t0 + 4 * u] = v[u];
         }
-        for (; t < n; t += 4) tile[(size_t)t * kEssRow + cc] = live ? col[(size_t)t * stride] : 0.0;
+        for (int t2 = n + (tid >> 5); t2 < S; t2 += 4) dst[t2] = 0.0;
     }
     __syncthreads();
-    const int sr = tid >> 2, q = tid & 3;                      // series (column) and lane within its group
-    double* zc = tile + sr;
+    const int sr = tid >> 2, q = tid & 3;                      // series and lane within its group
+    double* zc = tile + sr * S;
     const double nd = (double)n;
     double ss = 0.0, var_v = 0.0;
     if (q == 0) {
-        double sum = 0.0;                                      // mean (mean.jl:6), left to right
-        for (int64_t t = 0; t < n; ++t) sum = sum + zc[(size_t)t * kEssRow];
+        // mean (mean.jl:6), left to right; 16 steps of LDS reads in flight per block of the dependent adds
+        double sum = 0.0;
+        int t = 0;
+        for (; t + 16 <= n; t += 16) {
+            ess_f64x2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const ess_f64x2*>(zc + t + 2 * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sum = (sum + v[u].x) + v[u].y;
+        }
+        for (; t < n; ++t) sum = sum + zc[t];
         const double mean = sum / nd;
-        if (a.vtype == 3) var_v = ess_bm([&](int64_t t) { return zc[(size_t)t * kEssRow]; }, n, a.batchlen);
-        for (int64_t t = 0; t < n; ++t) {
-            const double z = zc[(size_t)t * kEssRow] - mean;
-            zc[(size_t)t * kEssRow] = z;
+        if (a.vtype == 3) var_v = ess_bm([&](int64_t t) { return zc[t]; }, (int64_t)n, a.batchlen);
+        // centre in place; ss = sum of z^2 with the lag sums' fma chain
+        for (t = 0; t + 16 <= n; t += 16) {
+            ess_f64x2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const ess_f64x2*>(zc + t + 2 * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                v[u].x = v[u].x - mean;
+                v[u].y = v[u].y - mean;
+                ss = __builtin_fma(v[u].x, v[u].x, ss);
+                ss = __builtin_fma(v[u].y, v[u].y, ss);
+                *reinterpret_cast<ess_f64x2*>(zc + t + 2 * u) = v[u];
+            }
+        }
+        for (; t < n; ++t) {
+            const double z = zc[t] - mean;
+            zc[t] = z;
             ss = __builtin_fma(z, z, ss);
         }
     }
@@ -114,29 +210,9 @@ __global__ __launch_bounds__(kEssThreads) void k_ess_tile(EssArgs a) {
         const int64_t k = (a.maxlag - 1) >= 0 ? (a.maxlag - 1) / 2 : -1;
         double gsum = 0.0, prev = 0.0;
         bool done = k < 0;
-        for (int64_t r0 = 0; !__all(done); r0 += 4) {
-            const int64_t jp = r0 + q;                         // this lane's pair
-            double g = 0.0;
-            if (!done && jp <= k) {
-                const int64_t L0 = 2 * jp, L1 = L0 + 1;        // lags; L1 <= maxlag <= n - 1
-                double s0 = 0.0, s1 = 0.0;
-                double b = zc[(size_t)L0 * kEssRow];           // z_{t+L0}
-                for (int64_t t = 0; t + L1 < n; ++t) {
-                    const double zt = zc[(size_t)t * kEssRow];
-                    const double b1 = zc[(size_t)(t + L1) * kEssRow];
-                    s0 = __builtin_fma(zt, b, s0);
-                    s1 = __builtin_fma(zt, b1, s1);
-                    b = b1;
-                }
-                s0 = __builtin_fma(zc[(size_t)(n - 1 - L0) * kEssRow], b, s0);   // lag L0's last term
-                g = s0 / nd + s1 / nd;                         // acv[2j] + acv[2j+1] (acv[0] = ss/n: the same sum)
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const double gi = __shfl(g, gl + i, 64);
-                if (!done) done = r0 + i > k || !geyer_take(gi, r0 + i, a.vtype, prev, gsum);
-            }
-        }
+        // round 0: one pair per lane (pairs 0-3; nearly independent draws stop there), then 4 pairs per lane
+        ess_round<2>(zc, n, nd, 0, q, gl, k, a.vtype, done, prev, gsum);
+        for (int64_t p0 = 4; !__all(done); p0 += 16) ess_round<8>(zc, n, nd, p0, q, gl, k, a.vtype, done, prev, gsum);
         var_v = (-acv0 + 2.0 * gsum) / nd;
     } else {
         var_v = __shfl(var_v, gl, 64);
@@ -202,7 +278,7 @@ hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t 
     using namespace mcmc;
     EssArgs a{samples, n, d, C, maxlag, batchlen, vtype, ess, var};
     if (n <= kEssTileMaxN) {
-        const size_t lds = (size_t)n * kEssRow * sizeof(double);
+        const size_t lds = (size_t)kEssTile * ess_stride((int)n) * sizeof(double);
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)k_ess_tile, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)lds);

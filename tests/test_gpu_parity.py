@@ -351,7 +351,7 @@ def test_model_released_before_its_chains(gpu):
 
 
 @pytest.mark.parametrize("vtype,name", [(1, "imse"), (2, "ipse"), (3, "bm")])
-@pytest.mark.parametrize("n", [90, 300])                  # LDS-staged series / global re-reads
+@pytest.mark.parametrize("n", [41, 90, 300, 618, 619])   # k_ess_tile (n <= 618, > 64 KB of LDS from 241) / k_ess_col
 def test_device_ess_bitwise(gpu, vtype, name, n):
     import torch
     rng = np.random.default_rng(n + vtype)
@@ -369,6 +369,24 @@ def test_device_ess_bitwise(gpu, vtype, name, n):
     xt = torch.from_numpy(x).cuda()
     got_d = mc.stats.ess_device(xt, name, batchlen=20)     # device pointers, no PCIe
     assert np.array_equal(got_d.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("n,maxlag", [(2, 0), (3, 0), (3, 1), (17, 5), (90, 6), (90, 7), (90, 89), (400, 9)])
+def test_device_ess_short_series_and_maxlag(gpu, n, maxlag):
+    """short series, maxlag below n - 1 (k = floor((maxlag - 1) / 2) pairs), white noise (Geyer stops at the first
+    pairs) next to strongly autocorrelated series (it runs to k), in one batch"""
+    rng = np.random.default_rng(n * 7 + maxlag)
+    d, C = 2, 200
+    x = rng.normal(size=(n, d, C))
+    for t in range(1, n):
+        x[t, 1] = 0.95 * x[t - 1, 1] + 0.1 * x[t, 1]
+    chain = type("Chain", (), {})()
+    chain._samples = x
+    for vtype, name in ((1, "imse"), (2, "ipse")):
+        ref, vref = orc.ess(x, vtype, maxlag, 0)
+        got, v = mc.stats.ess_device(chain, name, maxlag=maxlag, return_var=True)
+        assert np.array_equal(got.T.view(np.uint64), ref.view(np.uint64))
+        assert np.array_equal(v.T.view(np.uint64), vref.view(np.uint64))
 
 
 def test_device_ess_of_a_run(gpu):
