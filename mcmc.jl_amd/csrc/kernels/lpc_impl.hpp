@@ -21,12 +21,14 @@ __global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* x
 }
 
 // RWM for a handful of chains (C <= 64; config 1 is one chain), where one lane per chain leaves the chip idle
-// and each step is a chain of dependent operations: the Philox / Box-Muller work and the accept draw of the
-// next S = 256 / C steps of every chain are spread over the block's 256 threads (thread w: chain w % C, step
-// w / C) and staged in LDS, then lane c of wave 0 runs chain c's S accept steps from there.  rwm_body's
-// operations on the same values (x + RN(z scale), the short-circuit test against det_log(u)), so the chains are
-// bitwise the same.
+// and each step is a chain of dependent operations.  Wave 0's lane c runs chain c's accept chain; waves 1-3
+// (192 threads: thread g draws chain g % C, step g / C) produce the Philox / Box-Muller work and the accept
+// draw of the next S = 192 / C steps into the other half of a double-buffered LDS stage while wave 0 consumes
+// the current half, so the generation is off the dependent path.  Wave 0 prefetches step j+1's increments into
+// registers before it runs step j.  rwm_body's operations on the same values (x + RN(z scale), the
+// short-circuit test against det_log(u)), so the chains are bitwise the same.
 constexpr int kLaMaxChains = 64;
+constexpr int kLaGen = kBlock - 64;                  // generating threads
 template <int NB, class M, bool US>
 __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
     using P = LaneChain<NB, false>;
@@ -36,52 +38,78 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
     const M model(a.m);
     const Stream rs{s.key0, s.key1};
     const int C = (int)s.C;
-    const int S = kBlock / C;
-    __shared__ double dz_l[kBlock][NC];
-    __shared__ double lu_l[kBlock];
+    const int S = kLaGen / C;
+    __shared__ double dz_l[2][kLaGen][NC];
+    __shared__ double lu_l[2][kLaGen];
     const int w = (int)threadIdx.x;
-    double x[NC], sc[NC];
-    p.load(a.st.x, s.ld, x);
+    double sc[NC];
 #pragma unroll
     for (int k = 0; k < NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
-    double lp = p.load_scalar(a.st.lp);
-    // kept steps (kept_index) tracked incrementally: i_loc = burnin + 1 + kk thinning <= len; no 64-bit division
-    // on the dependent per-step path
-    const int64_t iloc0 = s.step_begin - s.run_step0;
-    int64_t kk_next = iloc0 > s.burnin + 1 ? (iloc0 - s.burnin - 1 + s.thinning - 1) / s.thinning : 0;
-    int64_t kept_next = s.burnin + 1 + kk_next * s.thinning;
-    for (int t0 = 0; t0 < s.nsteps; t0 += S) {
-        const int nb = s.nsteps - t0 < S ? s.nsteps - t0 : S;
-        const int sw = w / C, cw = w - sw * C;
-        if (sw < nb) {                               // RNG of (chain cw, step t0 + sw)
+    // waves 1-3: the increments randn(d) .* scale and log(rand()) of steps t0 .. t0 + S - 1 into half `buf`
+    auto generate = [&](int t0, int buf) {
+        const int g = w - 64;
+        const int sw = g / C, cw = g - sw * C;
+        if (sw < S && t0 + sw < s.nsteps) {
             const uint32_t chain = s.chain0 + (uint32_t)cw;
             const uint32_t i = (uint32_t)(s.step_begin + t0 + sw);
             double z[NC];
             gen_normals(p, rs, chain, i, z);
 #pragma unroll
-            for (int k = 0; k < NC; ++k) dz_l[w][k] = z[k] * sc[k];           // randn(d) .* scale
+            for (int k = 0; k < NC; ++k) dz_l[buf][g][k] = z[k] * sc[k];               // randn(d) .* scale
             const u32x4 u = rs.block(chain, i, 0u, TAG_ACCEPT);
-            lu_l[w] = det_log(uniform53(u.x, u.y));                             // log(rand())
+            lu_l[buf][g] = det_log(uniform53(u.x, u.y));                               // log(rand())
         }
-        __syncthreads();
-        if (w < 64) {                                // wave 0: lane c is chain c
+    };
+    double x[NC];
+    double lp = 0.0;
+    if (w < 64) {
+        p.load(a.st.x, s.ld, x);
+        lp = p.load_scalar(a.st.lp);
+    } else {
+        generate(0, 0);
+    }
+    __syncthreads();
+    // kept steps (kept_index) tracked incrementally: i_loc = burnin + 1 + kk thinning <= len; no 64-bit division
+    // on the dependent per-step path
+    const int64_t iloc0 = s.step_begin - s.run_step0;
+    int64_t kk_next = iloc0 > s.burnin + 1 ? (iloc0 - s.burnin - 1 + s.thinning - 1) / s.thinning : 0;
+    int64_t kept_next = s.burnin + 1 + kk_next * s.thinning;
+    const int item0 = p.live ? w : 0;               // lanes past the last chain replay chain 0 (nothing stored)
+    for (int r = 0, t0 = 0; t0 < s.nsteps; ++r, t0 += S) {
+        const int buf = r & 1;
+        if (w >= 64) {
+            if (t0 + S < s.nsteps) generate(t0 + S, buf ^ 1);
+        } else {
+            const int nb = s.nsteps - t0 < S ? s.nsteps - t0 : S;
+            double nz[NC], nl;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) nz[k] = dz_l[buf][item0][k];
+            nl = lu_l[buf][item0];
             for (int j = 0; j < nb; ++j) {
-                const int64_t i = s.step_begin + t0 + j;
-                const int item = p.live ? j * C + w : 0;
+                double dz[NC];
+#pragma unroll
+                for (int k = 0; k < NC; ++k) dz[k] = nz[k];
+                const double lu = nl;
+                if (j + 1 < nb) {                            // step j+1's increments, in flight during step j
+                    const int it = (j + 1) * C + item0;
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) nz[k] = dz_l[buf][it][k];
+                    nl = lu_l[buf][it];
+                }
                 double xp[NC];
 #pragma unroll
-                for (int k = 0; k < NC; ++k) xp[k] = x[k] + dz_l[item][k];     // pars + randn(d) .* scale
+                for (int k = 0; k < NC; ++k) xp[k] = x[k] + dz[k];                     // pars + randn(d) .* scale
                 bool oos;
                 const double lpp = eval_lp(p, model, xp, oos);
                 const double ratio = lpp - lp;
-                const bool acc = ratio > 0.0 || ratio > lu_l[item];             // RWM.jl:63
+                const bool acc = ratio > 0.0 || ratio > lu;                            // RWM.jl:63
                 if (acc) {
 #pragma unroll
                     for (int k = 0; k < NC; ++k) x[k] = xp[k];
                     lp = lpp;
                 }
-                const int64_t iloc = i - s.run_step0;
-                if (iloc == kept_next && iloc <= s.len) {                      // SerialMC.jl:49
+                const int64_t iloc = s.step_begin + t0 + j - s.run_step0;
+                if (iloc == kept_next && iloc <= s.len) {                            // SerialMC.jl:49
                     p.store_kept(s, kk_next, x, s.samples);
                     p.store_bit(s, kk_next, acc);
                     kk_next += 1;
@@ -91,9 +119,182 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
         }
         __syncthreads();
     }
-    p.store(a.st.x, s.ld, x);
-    p.store_t(a.st.lp, lp);
-    p.count_evals(s, s.nsteps);
+    if (w < 64) {
+        p.store(a.st.x, s.ld, x);
+        p.store_t(a.st.lp, lp);
+        p.count_evals(s, s.nsteps);
+    }
+}
+
+// RWM for one chain of d = D <= 4 (config 1: d = 3): path speculation.  The next 6 steps of the chain have 64
+// possible accept patterns; lane b of wave 0 assumes pattern b, so its states along those steps are known in
+// advance (x advances by its increment exactly at the steps b accepts) and it evaluates all 6 proposals without
+// waiting for any accept test -- six independent evaluations instead of a dependent chain.  A lane is
+// consistent when every accept test it computes agrees with its pattern; exactly one lane is (every lane agrees
+// with the true path up to its first difference from it, where the true test contradicts it), and its states
+// are the chain's: one ballot per 6 steps, and the winning lane index IS the accept pattern, so the new state is
+// read with v_readlane (no LDS round trip).  The arithmetic of every state, proposal and test is rwm_body's
+// (x + RN(z scale), the short-circuit test against det_log(u)) on the same values in the same order, so the chain
+// is bitwise the same.  D is exact (no per-coordinate validity masks).  Waves 1-3 produce the increments and
+// accept draws into a double-buffered LDS stage (as lpc_rwm_la), and copy the kept rows, staged in LDS by the
+// winning lane, out as contiguous runs during the next stage half.
+constexpr int kSpecK = 6;
+__device__ __forceinline__ double readlane_f64(double v, int lane) {   // lane: wave-uniform
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int D, class M, bool US>
+__global__ __launch_bounds__(kBlock) void lpc_rwm_spec(KernelArgs a) {
+    using P = LaneChain<1, false>;                   // RNG blocks of 4 normals: D <= 4 takes one
+    constexpr int NC = P::NC;
+    static_assert(D >= 1 && D <= NC, "one Philox block of normals per step");
+    const StepArgs& s = a.s;
+    const P p(s);                                    // stages the Box-Muller tables (every thread)
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    constexpr int S = kLaGen / kSpecK * kSpecK;      // steps per stage half: whole 6-step blocks
+    __shared__ double dz_l[2][kLaGen][D];
+    __shared__ double lu_l[2][kLaGen];
+    __shared__ double kept_l[2][kLaGen * D];         // kept rows of a half ([row][d]), rows kinfo_l[.][0] ..
+    __shared__ uint64_t kbits_l[2][kLaGen];          // and their accept words
+    __shared__ int64_t kinfo_l[2][2];                // first kept row, row count
+    const int w = (int)threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(w >> 6);   // wave-uniform role tests: scalar branches
+    double sc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) sc[k] = US ? s.scale1 : s.scale[k];
+    auto generate = [&](int t0, int buf) {           // waves 1-3: thread g draws step t0 + g
+        const int g = w - 64;
+        if (g < S && t0 + g < s.nsteps) {
+            const uint32_t i = (uint32_t)(s.step_begin + t0 + g);
+            double z[NC];
+            gen_normals(p, rs, s.chain0, i, z);
+#pragma unroll
+            for (int k = 0; k < D; ++k) dz_l[buf][g][k] = z[k] * sc[k];                // randn(d) .* scale
+            const u32x4 u = rs.block(s.chain0, i, 0u, TAG_ACCEPT);
+            lu_l[buf][g] = det_log(uniform53(u.x, u.y));                               // log(rand())
+        }
+    };
+    auto flush = [&](int buf, int t, int nt) {       // threads t, t+nt, ... copy half buf's kept rows out
+        const int64_t k0 = kinfo_l[buf][0], nr = kinfo_l[buf][1];
+        if (s.samples != nullptr) {
+            double* dst = s.samples + (size_t)k0 * D;
+            for (int64_t e = t; e < nr * D; e += nt) dst[e] = kept_l[buf][e];
+        }
+        if (s.acc_bits != nullptr)
+            for (int64_t e = t; e < nr; e += nt) s.acc_bits[(size_t)(k0 + e) * (size_t)s.nw] = kbits_l[buf][e];
+    };
+    double x[D];                                     // wave 0: the chain's state (uniform)
+    double lp = 0.0;
+    if (wave == 0) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = a.st.x[(size_t)k * (size_t)s.ld];
+        lp = a.st.lp[0];
+    } else {
+        generate(0, 0);
+    }
+    __syncthreads();
+    const int64_t iloc0 = s.step_begin - s.run_step0;
+    int64_t kk_next = iloc0 > s.burnin + 1 ? (iloc0 - s.burnin - 1 + s.thinning - 1) / s.thinning : 0;
+    int64_t kept_next = s.burnin + 1 + kk_next * s.thinning;
+    const int b = w & 63;                            // wave 0: this lane's accept pattern
+    int r = 0;
+    for (int t0 = 0; t0 < s.nsteps; ++r, t0 += S) {
+        const int buf = r & 1;
+        if (wave != 0) {
+            if (r > 0) flush(buf ^ 1, w - 64, kLaGen);      // the previous half's kept rows
+            if (t0 + S < s.nsteps) generate(t0 + S, buf ^ 1);
+        } else {
+            const int nb = s.nsteps - t0 < S ? s.nsteps - t0 : S;
+            const int64_t kfirst = kk_next;
+            for (int j0 = 0; j0 < nb; j0 += kSpecK) {
+                const int kb = nb - j0 < kSpecK ? nb - j0 : kSpecK;   // steps in this block (uniform)
+                // the block's kept steps (SerialMC.jl:49): bit i of km
+                uint32_t km = 0;
+                {
+                    const int64_t base = iloc0 + t0 + j0;            // i_loc of the block's first step
+                    const int64_t end = base + kb - 1 < s.len ? base + kb - 1 : s.len;   // last keepable i_loc
+                    if (kept_next <= end) {
+                        if (s.thinning == 1) {                       // a contiguous run: bits first .. last
+                            const int f = (int)(kept_next - base), l = (int)(end - base);
+                            km = ((2u << l) - 1u) & ~((1u << f) - 1u);
+                            kept_next = end + 1;
+                        } else {
+                            for (; kept_next <= end; kept_next += s.thinning) km |= 1u << (int)(kept_next - base);
+                        }
+                    }
+                }
+                // all 6 steps unconditionally (no branch between the LDS reads and the arithmetic): the stage rows of
+                // steps past kb lie inside the stage (S is a multiple of 6) and only patterns with zero bits there can
+                // be consistent, so those steps neither move xs nor decide ok
+                bool ok = (b >> kb) == 0;                           // patterns past the block's end: not a path
+                double xs[D], xh[kSpecK][D];
+                double lps = lp;
+#pragma unroll
+                for (int k = 0; k < D; ++k) xs[k] = x[k];
+#pragma unroll
+                for (int i = 0; i < kSpecK; ++i) {
+                    const int it = j0 + i;
+                    const double lu = lu_l[buf][it];
+                    double xp[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) xp[k] = xs[k] + dz_l[buf][it][k];       // pars + randn(d) .* scale
+                    double acc0 = 0.0;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) model.acc(acc0, xp[k]);
+                    bool oos;
+                    const double lpp = llacc_finish(model, acc0, oos);                 // model.eval
+                    const double ratio = lpp - lps;
+                    const bool acc = (ratio > 0.0) | (ratio > lu);                       // RWM.jl:63
+                    const bool bi = (b >> i) & 1;
+                    ok = ok && (acc == bi || i >= kb);
+#pragma unroll
+                    for (int k = 0; k < D; ++k) xs[k] = bi ? xp[k] : xs[k];
+                    lps = bi ? lpp : lps;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) xh[i][k] = xs[k];
+                }
+                const uint64_t okm = __ballot(ok);
+                const int src = okm ? __builtin_ctzll(okm) : 0;      // the consistent lane = the accept pattern
+#pragma unroll
+                for (int k = 0; k < D; ++k) x[k] = readlane_f64(xs[k], src);
+                lp = readlane_f64(lps, src);
+                if (km && b == src) {                                // the consistent lane stages the kept rows
+                    int kr = (int)(kk_next - kfirst);
+#pragma unroll
+                    for (int i = 0; i < kSpecK; ++i) {
+                        if ((km >> i) & 1u) {
+#pragma unroll
+                            for (int k = 0; k < D; ++k) kept_l[buf][kr * D + k] = xh[i][k];
+                            kbits_l[buf][kr] = (uint64_t)((src >> i) & 1);
+                            kr += 1;
+                        }
+                    }
+                }
+                kk_next += __builtin_popcount(km);
+            }
+            if (w == 0) {
+                kinfo_l[buf][0] = kfirst;
+                kinfo_l[buf][1] = kk_next - kfirst;
+            }
+        }
+        __syncthreads();
+    }
+    if (r > 0) flush((r - 1) & 1, w, kBlock);            // the last half, by the whole block
+    if (w == 0) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) a.st.x[(size_t)k * (size_t)s.ld] = x[k];
+        a.st.lp[0] = lp;
+        if (s.n_evals != nullptr) atomicAdd(s.n_evals, (unsigned long long)s.nsteps);
+    }
+}
+
+template <int D, class M>
+static void lpc_spec_launch(const KernelArgs& a, hipStream_t st) {
+    if (a.s.scale_uniform) lpc_rwm_spec<D, M, true><<<1, kBlock, 0, st>>>(a);
+    else lpc_rwm_spec<D, M, false><<<1, kBlock, 0, st>>>(a);
 }
 
 template <int NB, bool F, class M>
@@ -103,6 +304,16 @@ static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
     const char* us = a.s.scale_uniform ? "true" : "false";
     switch (a.sa.kind) {
         case SK_RWM:
+            if (NB == 1 && a.s.C == 1) {
+                mcmc_note_step_kernel("lpc_rwm_spec<%d, %s, %s>", (int)a.s.d, M::kName, us);
+                switch (a.s.d) {
+                    case 1: lpc_spec_launch<1, M>(a, st); break;
+                    case 2: lpc_spec_launch<2, M>(a, st); break;
+                    case 3: lpc_spec_launch<3, M>(a, st); break;
+                    default: lpc_spec_launch<4, M>(a, st); break;
+                }
+                break;
+            }
             if (a.s.C <= kLaMaxChains) {
                 mcmc_note_step_kernel("lpc_rwm_la<%d, %s, %s>", NB, M::kName, us);
                 if (a.s.scale_uniform) lpc_rwm_la<NB, M, true><<<1, kBlock, 0, st>>>(a);

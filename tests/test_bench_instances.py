@@ -7,7 +7,8 @@ run those workloads' own configurations, read back which step kernel ran (`mcmc_
 compare the HIP results with the oracle bit for bit:
 
 - config 2 (d=3) -> `lpc_rwm<1, false, IsoDot, true>`; the metric (d=32) -> `lpc_rwm<8, true, IsoDot, true>`;
-- config 1 (one chain) and C <= 64 -> the look-ahead kernel `lpc_rwm_la`, also across launches
+- config 1 (one chain, d <= 4) -> the path-speculation kernel `lpc_rwm_spec`; C <= 64 -> the
+  look-ahead kernel `lpc_rwm_la`; both also across launches
   (`steps_per_launch`) and continued runs, where a launch starts mid-way through the kept range;
 - the metric at its full size: 2^20 chains, d=32, SerialMC(1000, 100, 10) with device-resident outputs,
   checked bitwise on 4 096 chains spread over the batch and on every chain's accept bits' statistics.
@@ -60,10 +61,12 @@ def test_nonuniform_scale_takes_the_generic_instance(gpu):
 
 @pytest.mark.parametrize("uniform", [True, False])
 @pytest.mark.parametrize("spl", [0, 1, 7])
-@pytest.mark.parametrize("C", [1, 37, 64])
+@pytest.mark.parametrize("C", [1, 2, 5, 32, 33, 37, 64])
 def test_lookahead_rwm_across_launches_and_runs(gpu, C, spl, uniform):
-    """lpc_rwm_la (C <= 64): with steps_per_launch 1 or 7 and a continued run, launches begin inside the kept
-    range (lpc_impl.hpp: the kept-step counter restarts from step_begin - run_step0 > burnin + 1)."""
+    """few-chain RWM kernels: lpc_rwm_spec (one chain, d <= 4: path speculation, 6 steps per block, blocks cut
+    by launch boundaries) and lpc_rwm_la (C <= 64).  With steps_per_launch 1 or 7 and a continued
+    run, launches begin inside the kept range (the kept-step counter restarts from step_begin - run_step0 >
+    burnin + 1)."""
     d = 3
     m = (_readme_model(d) if uniform else
          mc.model(mc.IsoNormalDot(), init=np.ones(d), scale=np.array([0.8, 1.0, 1.3])))
@@ -71,7 +74,8 @@ def test_lookahead_rwm_across_launches_and_runs(gpu, C, spl, uniform):
     t = (m * mc.RWM(0.1) * r).batch(C, seed=3, steps_per_launch=spl)
     c1 = mc.run(t)
     c2 = mc.run(c1)                                               # runners.jl:14: the same chains continue
-    assert t.step_kernel == f"lpc_rwm_la<1, IsoDot, {'true' if uniform else 'false'}>"
+    us = "true" if uniform else "false"
+    assert t.step_kernel == (f"lpc_rwm_spec<3, IsoDot, {us}>" if C == 1 else f"lpc_rwm_la<1, IsoDot, {us}>")
     oc = orc.OracleChains(m, mc.RWM(0.1), nchains=C, seed=3)
     s1, _, a1 = oc.run(r)
     s2, _, a2 = oc.run(r)
@@ -85,7 +89,7 @@ def test_readme_config1_instance(gpu):
     m1 = _readme_model(3)
     t = (m1 * mc.RWM(0.1) * mc.SerialMC(steps=1000, burnin=100)).batch(1, seed=1)
     ch = mc.run(t)
-    assert t.step_kernel == "lpc_rwm_la<1, IsoDot, true>"
+    assert t.step_kernel == "lpc_rwm_spec<3, IsoDot, true>"
     oc = orc.OracleChains(m1, mc.RWM(0.1), nchains=1, seed=1)
     s, _, acc = oc.run(mc.SerialMC(steps=1000, burnin=100))
     _check(ch, s, acc)
@@ -153,3 +157,23 @@ def test_full_size_metric_run(gpu):
     assert np.all(np.abs(mean_all - sub.mean(axis=1)) < 6 * se_mean)
     assert np.all(np.abs(var_all / sub.var(axis=1) - 1) < 6 * np.sqrt(2 / sub.shape[1]))
     assert bool(torch.isfinite(samples).all())
+
+
+@pytest.mark.parametrize("d", [1, 3, 4, 5, 8, 9])
+@pytest.mark.parametrize("C", [1, 3, 16])
+def test_few_chain_rwm_models_and_sizes(gpu, C, d):
+    """the few-chain kernels on every separable model, d across the lpc_rwm_spec / lpc_rwm_la boundary (d <= 4),
+    out-of-support proposals included (AbsNormal's -Inf branch does not arise; DistDSL Gamma rejects x <= 0)"""
+    models = [mc.model(mc.IsoNormalDot(), init=np.linspace(0.5, 1.5, d), grad=True),
+              mc.model(mc.NormalDSL(0.3, 1.7), v=np.linspace(-1, 1, d), gradient=True),
+              mc.model(mc.DistDSL("Gamma", 3, 0.2), x=np.full(d, 0.6), gradient=True)]
+    r = mc.SerialMC(steps=97, burnin=9, thinning=4)
+    for m in models:
+        sp = mc.RWM(0.4)
+        ch = mc.run((m * sp * r).batch(C, seed=8))
+        assert ch.task.step_kernel.startswith("lpc_rwm_spec" if d <= 4 and C == 1 else "lpc_rwm_la")
+        oc = orc.OracleChains(m, mc.RWM(0.4), nchains=C, seed=8)
+        s, _, acc = oc.run(r)
+        _check(ch, s, acc)
+        assert np.array_equal(ch.final_x, oc.x) and np.array_equal(ch.final_lp, oc.lp)
+        assert ch.task.evals == C * 97
