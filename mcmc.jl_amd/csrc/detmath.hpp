@@ -310,7 +310,25 @@ struct LogTState {
     dm_f64x2 a, t;
     int e;
 };
+#ifndef GLM_LOG_FREXP
+#define GLM_LOG_FREXP 0
+#endif
 __device__ __forceinline__ void det_log_tab_s1(double v, LogTState& L, const double (*tab)[4] = kBmLogTab) {
+#if GLM_LOG_FREXP
+    // round-1 experiment, rebuilt for the fault investigation (not the shipped form): exponent and
+    // mantissa from the hardware frexp, v = mh 2^eh with mh in [0.5, 1); m' = 2 mh in [1, 2) as below
+    const double mh = __builtin_amdgcn_frexp_mant(v);
+    const int eh = __builtin_amdgcn_frexp_exp(v);
+    const uint64_t b = d2bits(mh);
+    const uint32_t top7 = (uint32_t)(b >> 45) & 0x7fu;
+    const uint32_t up = top7 >> 6;
+    L.e = eh - 1 + (int)up;
+    L.m = bits2d((b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52));
+    const dm_f64x2* row = reinterpret_cast<const dm_f64x2*>(tab[top7]);
+    L.a = row[0];
+    L.t = row[1];
+    L.v = v;
+#else
     const bool sub = v < 0x1p-1022;                                  // zero or subnormal
     const double xs = sub ? v * 0x1p54 : v;
     const uint64_t b = d2bits(xs);
@@ -322,6 +340,7 @@ __device__ __forceinline__ void det_log_tab_s1(double v, LogTState& L, const dou
     L.a = row[0];                                                    // (inv_c, T_hi)
     L.t = row[1];                                                    // (T_lo, 0)
     L.v = v;
+#endif
 }
 __device__ __forceinline__ void det_log_tab_s2(LogTState& L) {
     const double r = __builtin_fma(L.m, L.a.x, -1.0);
