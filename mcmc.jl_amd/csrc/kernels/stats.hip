@@ -226,6 +226,94 @@ __global__ __launch_bounds__(kEssThreads) void k_ess_tile(EssArgs a) {
     }
 }
 
+// Series of up to N = 32, 64 or 96 kept samples, IMSE/IPSE (the metric keeps 90): one lane per series, the whole
+// series in registers.  A wave covers 64 consecutive chains of one parameter, so every load of a step is one
+// coalesced 512-byte row; no LDS, no staging round trip, no cross-lane traffic: the mean, the centring and the
+// sums of squares run on every lane, and each lane scans its own pairs.  Lag sums go two pairs (four lags, four
+// independent fma chains) per step; the wave leaves the unrolled pair loop once all its series have met their
+// first non-positive pair (or k), so a wave pays for its slowest series only -- against k_ess_tile's fixed rounds of
+// sixteen pairs.  N - 32 < n <= N (N = 32: 2 <= n <= 32): positions t >= n hold exact zeros, which leave every sum
+// unchanged (s + 0 = s and fma(z, 0, s) = s, s never being -0), so the arithmetic is k_ess_tile's (and orc_ess's)
+// bit for bit: left-to-right sum, ss and every lag sum an fma chain in t order.
+template <int N>
+__global__ __launch_bounds__(256, 2) void k_ess_reg(EssArgs a) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t j = blockIdx.y;
+    const bool live = c < a.C;
+    const int n = (int)a.n;
+    const size_t stride = (size_t)a.d * (size_t)a.C;
+    const double* col = a.s + (size_t)j * (size_t)a.C + (size_t)(live ? c : 0);
+    double z[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        if (t < N - 32) {
+            z[t] = col[(size_t)t * stride];
+        } else {                                               // the last 32 positions: rows past n read row n-1
+            const double v = col[(size_t)(t < n ? t : n - 1) * stride];
+            z[t] = t < n ? v : 0.0;
+        }
+    }
+    const double nd = (double)n;
+    // s / n for the autocovariances: q0 = RN(s rn), then one correction with the exact residual (fma).  With rn the
+    // correctly rounded 1/n and q0 faithful, q0 + (s - n q0) rn rounds to the correctly rounded s / n (Markstein's
+    // theorem; no underflow here): the IEEE quotient orc_ess computes, for 3 operations instead of the ~11 of a
+    // division (tests/test_oracle.py checks the identity on half a billion quotients, near-exact ones included).
+    const double rn = 1.0 / nd;
+    auto qdiv = [&](double x) {
+        const double q0 = x * rn;
+        return __builtin_fma(__builtin_fma(-q0, nd, x), rn, q0);
+    };
+    double sum = 0.0;
+#pragma unroll
+    for (int t = 0; t < N; ++t) sum = sum + z[t];              // mean.jl:6, left to right; the zero pad adds +0
+    const double mean = sum / nd;
+#pragma unroll
+    for (int t = 0; t < N; ++t) z[t] = (t < N - 32 || t < n) ? z[t] - mean : 0.0;
+    // the lag-0 sum is ss (the same fma chain): it runs as the first of step 0's four chains
+    double ss = 0.0, acv0 = 0.0;
+    const int64_t k = (a.maxlag - 1) >= 0 ? (a.maxlag - 1) / 2 : -1;
+    double gsum = 0.0, prev = 0.0;
+    bool done = k < 0 || !live;
+#pragma unroll
+    for (int jp = 0; jp < N / 2; jp += 2) {                    // pairs jp, jp + 1: lags 2 jp .. 2 jp + 3
+        if (jp > 0 && __ballot(!done) == 0) break;
+        double sl[4] = {0.0, 0.0, 0.0, 0.0};
+        auto lag_terms = [&](int t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int L = 2 * jp + i;
+                if (t + L < N) sl[i] = __builtin_fma(z[t], z[t + L], sl[i]);
+            }
+        };
+        // t in blocks of 4; once z[t + 2 jp] can be the zero pad (t + 2 jp >= N - 32), a block starting at or past
+        // n - 2 jp (a uniform test) ends the sums: every term left is fma(z, 0, s) = s
+#pragma unroll
+        for (int tb = 0; tb < N; tb += 4) {
+            if (tb + 2 * jp >= N - 32 && tb + 2 * jp >= n) break;
+#pragma unroll
+            for (int t = tb; t < tb + 4; ++t) lag_terms(t);
+        }
+        if (jp == 0) {
+            ss = sl[0];
+            acv0 = qdiv(ss);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int jj = jp + h;
+            if (jj >= N / 2) break;
+            const double g = (jj == 0 ? acv0 : qdiv(sl[2 * h])) + qdiv(sl[2 * h + 1]);   // acv[2j] + acv[2j+1]
+            if (!done) done = jj > k || !geyer_take(g, jj, a.vtype, prev, gsum);
+        }
+    }
+    if (live) {
+        const double var_v = (-acv0 + 2.0 * gsum) / nd;
+        const double var_iid = (ss / (nd - 1.0)) / nd;
+        const size_t o = (size_t)j * (size_t)a.C + (size_t)c;
+        a.ess[o] = (nd * var_iid) / var_v;                      // ess.jl:9
+        if (a.var) a.var[o] = var_v;
+    }
+}
+
 // long series (n > kEssTileMaxN): one thread per series, the column re-read from global memory per lag
 __global__ __launch_bounds__(kEssBlock) void k_ess_col(EssArgs a) {
     const int64_t c = (int64_t)blockIdx.x * kEssBlock + threadIdx.x;
@@ -277,7 +365,12 @@ hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t 
                            int64_t batchlen, double* ess, double* var, hipStream_t st) {
     using namespace mcmc;
     EssArgs a{samples, n, d, C, maxlag, batchlen, vtype, ess, var};
-    if (n <= kEssTileMaxN) {
+    if (vtype != 3 && n <= 96) {
+        const dim3 grid((unsigned)((C + 255) / 256), (unsigned)d);
+        if (n <= 32) k_ess_reg<32><<<grid, 256, 0, st>>>(a);
+        else if (n <= 64) k_ess_reg<64><<<grid, 256, 0, st>>>(a);
+        else k_ess_reg<96><<<grid, 256, 0, st>>>(a);
+    } else if (n <= kEssTileMaxN) {
         const size_t lds = (size_t)kEssTile * ess_stride((int)n) * sizeof(double);
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)k_ess_tile, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -351,7 +351,9 @@ def test_model_released_before_its_chains(gpu):
 
 
 @pytest.mark.parametrize("vtype,name", [(1, "imse"), (2, "ipse"), (3, "bm")])
-@pytest.mark.parametrize("n", [41, 90, 300, 618, 619])   # k_ess_tile (n <= 618, > 64 KB of LDS from 241) / k_ess_col
+# k_ess_reg<32/64/96> (n <= 96, IMSE/IPSE; 32 and 64 at the bucket edges), k_ess_tile (batch means, 96 < n <= 618,
+# > 64 KB of LDS from 241) / k_ess_col
+@pytest.mark.parametrize("n", [20, 32, 33, 41, 64, 65, 90, 96, 97, 300, 618, 619])
 def test_device_ess_bitwise(gpu, vtype, name, n):
     import torch
     rng = np.random.default_rng(n + vtype)
@@ -361,17 +363,19 @@ def test_device_ess_bitwise(gpu, vtype, name, n):
     x[0] = e[0]
     for t in range(1, n):
         x[t] = 0.6 * x[t - 1] + e[t]
-    ref, vref = orc.ess(x, vtype, 0, 20)
+    bl = 20 if n >= 40 else n // 2                          # batch means need two batches
+    ref, vref = orc.ess(x, vtype, 0, bl)
     chain = type("Chain", (), {})()
     chain._samples = x
-    got, v = mc.stats.ess_device(chain, name, batchlen=20, return_var=True)
+    got, v = mc.stats.ess_device(chain, name, batchlen=bl, return_var=True)
     assert np.array_equal(got.T, ref) and np.array_equal(v.T, vref)
     xt = torch.from_numpy(x).cuda()
-    got_d = mc.stats.ess_device(xt, name, batchlen=20)     # device pointers, no PCIe
+    got_d = mc.stats.ess_device(xt, name, batchlen=bl)     # device pointers, no PCIe
     assert np.array_equal(got_d.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("n,maxlag", [(2, 0), (3, 0), (3, 1), (17, 5), (90, 6), (90, 7), (90, 89), (400, 9)])
+@pytest.mark.parametrize("n,maxlag", [(2, 0), (3, 0), (3, 1), (17, 5), (64, 63), (65, 2), (90, 6), (90, 7), (90, 89),
+                                      (96, 95), (400, 9)])
 def test_device_ess_short_series_and_maxlag(gpu, n, maxlag):
     """short series, maxlag below n - 1 (k = floor((maxlag - 1) / 2) pairs), white noise (Geyer stops at the first
     pairs) next to strongly autocorrelated series (it runs to k), in one batch"""

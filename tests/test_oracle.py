@@ -406,6 +406,22 @@ def test_mala_logistic_recovers_posterior_mean():
     assert 0.2 < acc.mean() < 0.99
 
 
+def test_ess_quotient_is_ieee_division(tmp_path):
+    """k_ess_reg divides the autocovariance sums by n as two fmas around rn = 1/n (Markstein's correction); orc_ess
+    uses the IEEE division.  Bitwise the same on 4 million quotients (n = 1..1024, near-exact ones included); the
+    GPU ESS tests then compare the kernel with orc_ess on real series."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = os.path.join(os.path.dirname(__file__), "qdiv_check.c")
+    exe = str(tmp_path / "qdiv_check")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, src, "-lm"], check=True)
+    r = subprocess.run([exe, "1024", "4000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert "mismatches 0" in r.stdout
+
+
 @pytest.mark.parametrize("vtype,name", [(1, "imse"), (2, "ipse"), (3, "bm")])
 @pytest.mark.parametrize("phi", [0.0, 0.7, 0.95, -0.5])
 def test_oracle_ess_matches_numpy_stats(vtype, name, phi):
