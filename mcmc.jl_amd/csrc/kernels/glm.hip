@@ -52,6 +52,11 @@ constexpr bool kGlmFence = GLM_FENCE != 0;
 #define GLM_GFENCE 1
 #endif
 constexpr bool kGlmGFence = GLM_GFENCE != 0;
+// 1 (default): single-slice MALA runs the wave-specialised glm_mala1ws (M and V waves paired on each SIMD);
+// 0: glm_mala1 (one wave per tile does both)
+#ifndef GLM_MALA1_WS
+#define GLM_MALA1_WS 1
+#endif
 // NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
 
 struct GlmShape {
@@ -1019,6 +1024,368 @@ __global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
     glm_count_evals(a, p, s.nsteps);
 }
 
+// ------------------------------------------------------------------ wave-specialised single-slice MALA
+// glm_mala1ws<NM>: glm_mala1's step (config 3: logistic MALA, d = 128) with the work of a 16-chain tile split over
+// two waves that share a SIMD (a 512-thread workgroup puts waves w and w + 4 on one SIMD):
+//   wave w < 4   ("M", matrix): holds the tile's proposal (the B operands) and the gradient accumulators in registers
+//                and issues every MFMA: eta_{t+1} = X_{t+1} beta and G += X_{t-1}^T r_{t-1};
+//   wave w + 4   ("V", vector): the proposal (Philox, Box-Muller, MALA.jl:98-103), the X tile loads and, per
+//                observation tile, the elementwise log-likelihood terms and residual weights r_t on eta_t.
+// eta_t and r_t cross through LDS (double-buffered), one barrier per tile.  The fp64 matrix and vector pipes of a
+// SIMD run concurrently for different waves (scripts/peak_f64.hip: MFMA-only and FMA-only waves paired on a SIMD
+// take max, not sum, of their times), whereas glm_mala1's single wave per SIMD (300 VGPRs) serialises its VALU
+// work with its MFMAs.  Every sum is formed by the same instructions in the same order as glm_mala1 (eta chains
+// over (m, e, q); G chains over observations; a lane's likelihood terms in (t, r) order; qf / qb / prior as
+// there), so the results are glm_mala1's bit for bit and orc_glm_eval restates them.
+// LDS (doubles; XS = 16 lds_stride): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
+// which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | tables | qf, lik [2][4][16].
+template <int NM>
+__host__ __device__ constexpr int glm_ws_region(int XS) {
+    return (2 * XS + 4096) > (4 * 4 * NM * 64) ? (2 * XS + 4096) : (4 * 4 * NM * 64);
+}
+__host__ __device__ inline size_t glm_ws_lds_doubles(int nm, int lds_stride) {
+    const int XS = 16 * lds_stride;
+    const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
+    return (size_t)(2 * XS + R + 4 * 16 + 4 * 128 + 2 * 64 + 2 * 4 * 16);
+}
+template <int NM>
+__global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int NS = 4 * NM;
+    constexpr int KM = 4 * NM;
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const ModelArgs& M = a.m;
+    const GlmShape& g = a.g;
+    const int wv = (int)(threadIdx.x >> 6);
+    const bool vwave = __builtin_amdgcn_readfirstlane(wv) >= 4;
+    GlmPos p;
+    p.lane = threadIdx.x & 63;
+    p.q = p.lane >> 4;
+    p.cl = p.lane & 15;
+    p.tile = wv & 3;
+    p.wave = p.tile;
+    p.slice = 0;
+    p.base = 0;
+    p.c = ((int64_t)blockIdx.x * 4 + p.tile) * 16 + p.cl;
+    p.live = p.c < s.C;
+    const int S = g.lds_stride;
+    const int XS = 16 * S;
+    double* const Xs = smem;                                   // 4 X tile slots: 0, 1 here, 2, 3 in region R
+    double* const R = smem + 2 * XS;
+    double* const Eb = R + 2 * XS;                             // eta [2][4 tiles][64 lanes][4]
+    double* const Rb = Eb + 2048;                              // r   [2][4 tiles][64 lanes][4]
+    double* const beta = R;                                    // proposal [4 tiles][NS][64] (proposal phase only)
+    double* const Yb = R + glm_ws_region<NM>(XS);              // Y [4][16]
+    double* const ltabp = Yb + 64;                             // logistic tables: log [128][4], exp [64][2]
+    double* const qfl = ltabp + 4 * 128 + 2 * 64;              // qf [4][16], then lik [4][16]
+    double* const likl = qfl + 64;
+    auto xslot = [&](int64_t tt) -> double* { const int b = (int)(tt & 3); return b < 2 ? Xs + b * XS : R + (b - 2) * XS; };
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int64_t cc = p.live ? p.c : 0;
+    const size_t ld = (size_t)s.ld;
+    const double* const xl = glm_lane_ptr(p, a.st.x, s.ld, cc);
+    const double* const gl = glm_lane_ptr(p, a.st.g, s.ld, cc);
+    const int64_t i = s.step_begin;                            // ONE step per launch (as glm_mala1)
+    const double h = sa.tuner ? a.st.t_step[cc] : sa.drift_step;
+    const double half = h / 2.0;
+    const double twoh = 2.0 * h;
+    const double Lc = det_log(kTwoPi * h) / 2.0;
+    const int64_t ntiles = g.n_pad / 16;
+    const bool logi = M.kind == MK_LOGISTIC;
+    // X / Y tile transfer, by the 256 threads of one wave role (u = thread index within the role)
+    constexpr int kHalf = 16 * 8 * NM;                         // f64x2 per tile (d_pad = 16 NM)
+    constexpr int kPer = (kHalf + 255) / 256;
+    constexpr int kLgHalfrow = __builtin_ctz(8 * NM);
+    const int u = (int)(threadIdx.x & 255);
+    f64x2 xbuf[kPer];
+    double ybuf = 0.0;
+    auto load_tile = [&](int64_t tt) {
+        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * 16 * g.d_pad);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int e = u + 256 * j;
+            xbuf[j] = src[e < kHalf ? e : 0];
+        }
+        ybuf = (u < 16) ? M.Y[tt * 16 + u] : 0.0;
+    };
+    auto store_tile = [&](int64_t tt) {
+        double* Xb = xslot(tt);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int e = u + 256 * j;
+            if (e < kHalf) {
+                const int row = e >> kLgHalfrow, col = 2 * (e & ((1 << kLgHalfrow) - 1));
+                *reinterpret_cast<f64x2*>(&Xb[row * S + col]) = xbuf[j];
+            }
+        }
+        if (u < 16) Yb[(tt & 3) * 16 + u] = ybuf;
+    };
+    double* const xb = beta + (size_t)(p.tile * NS) * 64 + p.lane;   // this lane's proposal slots
+
+    // ---- proposal phase: V waves draw the proposal (MALA.jl:98-103) into LDS; M waves stage X tiles 0 and 1
+    if (vwave) {
+        double qf = 0.0;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const uint32_t blk = (uint32_t)(4 * m + p.q);                    // coords 4*blk .. 4*blk+3
+            const u32x4 w = rs.block(chain, (uint32_t)i, blk, TAG_NORMAL);
+            double z[4];
+            normals4(w, z[0], z[1], z[2], z[3]);
+            const double sq = __builtin_sqrt(h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int slot = 4 * m + e;
+                const bool v = glm_valid(a, p, slot);
+                const size_t o = (size_t)(16 * m + e) * ld;
+                const double xv = v ? xl[o] : 0.0;
+                const double gv = v ? gl[o] : 0.0;
+                const double pm = xv + half * gv;                               // MALA.jl:98
+                const double xpv = pm + sq * (v ? z[e] : 0.0);                  // MALA.jl:100
+                const double ee = pm - xpv;
+                if (v) qf = qf + ((-(ee * ee)) / twoh - Lc);                    // MALA.jl:103
+                xb[64 * slot] = xpv;
+            }
+        }
+        qf = glm_sum(a, p, GlmLds{}, qf);
+        if (p.q == 0) qfl[p.tile * 16 + p.cl] = qf;
+        if (logi) {
+            for (int e = u; e < 4 * 128 + 2 * 64; e += 256)
+                ltabp[e] = e < 4 * 128 ? (&kBmLogTab[0][0])[e] : (&kExp2Tab[0][0])[e - 4 * 128];
+        }
+    } else {
+        load_tile(0);
+        store_tile(0);
+        if (ntiles > 1) {
+            load_tile(1);
+            store_tile(1);
+        }
+    }
+    __syncthreads();
+    // ---- M: the proposal into registers, eta_0;  V: X tile 2 into registers (slot 2 overlays the proposal)
+    double bx[NS];
+    f64x4 G[NM];
+    if (!vwave) {
+#pragma unroll
+        for (int slot = 0; slot < NS; ++slot) bx[slot] = xb[64 * slot];
+#pragma unroll
+        for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
+    } else if (ntiles > 2) {
+        load_tile(2);
+    }
+    __syncthreads();                                           // the proposal area is free from here on
+    f64x4* const Eq = reinterpret_cast<f64x4*>(Eb) + p.tile * 64 + p.lane;   // + 256 * buffer
+    f64x4* const Rq = reinterpret_cast<f64x4*>(Rb) + p.tile * 64 + p.lane;
+    auto eta_of = [&](int64_t tt) {                            // glm_eval1_tiles' eta chain, operands read ahead
+        const double* xrow = xslot(tt) + p.cl * S + 4 * p.q;
+        constexpr int kLA = 4;
+        double av[KM];
+#pragma unroll
+        for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow[16 * (m >> 2) + (m & 3)];
+        f64x4 e = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int m = 0; m < KM; ++m) {
+            if (m + kLA < KM) av[m + kLA] = xrow[16 * ((m + kLA) >> 2) + ((m + kLA) & 3)];
+            e = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bx[m], e, 0, 0, 0);
+        }
+        return e;
+    };
+    auto g_of = [&](int64_t tt) {                              // G += X_tt^T r_tt (glm_eval1_tiles' G product)
+        const f64x4 rv = Rq[256 * (tt & 1)];
+        const double* gcol = xslot(tt) + 4 * (p.cl & 3) + (p.cl >> 2);
+        double ga[NM];
+#pragma unroll
+        for (int T = 0; T < NM; ++T) ga[T] = gcol[p.q * S + 16 * T];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            double gn[NM];
+            if (kk < 3) {
+#pragma unroll
+                for (int T = 0; T < NM; ++T) gn[T] = gcol[(4 * (kk + 1) + p.q) * S + 16 * T];
+            }
+#pragma unroll
+            for (int T = 0; T < NM; ++T) G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[T], rv[kk], G[T], 0, 0, 0);
+            if (kk < 3) {
+#pragma unroll
+                for (int T = 0; T < NM; ++T) ga[T] = gn[T];
+            }
+        }
+    };
+    if (!vwave) Eq[0] = eta_of(0);
+    __syncthreads();
+    // ---- the observation tiles
+    const double sgn = M.link_sign;
+    const double sn = M.noise_sigma, s2n = sn * sn;
+    const double logsn = logi ? 0.0 : det_log(sn);
+    const double isn = 1.0 / sn, is2n = 1.0 / s2n;
+    const double (*ltab)[4] = reinterpret_cast<const double (*)[4]>(ltabp);
+    const double (*etab)[2] = reinterpret_cast<const double (*)[2]>(ltabp + 4 * 128);
+    const int64_t nfull = M.n / 16;
+    // one loop per role, each with one barrier per tile (the same count): the roles' loop invariants (the V waves'
+    // polynomial constants, the M waves' operand addresses) stay out of each other's register pressure
+    double lik_part = 0.0;
+    if (!vwave) {
+        for (int64_t t = 0; t < ntiles; ++t) {
+            if (t + 1 < ntiles) Eq[256 * ((t + 1) & 1)] = eta_of(t + 1);
+            if (t >= 1) g_of(t - 1);
+            __syncthreads();
+        }
+    } else {
+        for (int64_t t = 0; t < ntiles; ++t) {
+            if (t + 2 < ntiles) {                              // slot (t+2) % 4 held tile t-2: read before the last barrier
+                store_tile(t + 2);
+                if (t + 3 < ntiles) load_tile(t + 3);
+            }
+            const f64x4 eta = Eq[256 * (t & 1)];
+            const double* LY = Yb + (t & 3) * 16;
+            double y[4], pr[4], term[4], rv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
+            if (logi) {
+                ExpTState E[4];
+                LogTState Lg[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) det_exp_tab_s1(-(sgn * eta[r]), E[r], etab);   // prob = 1/(1+exp(-X*vars))
+#pragma unroll
+                for (int r = 0; r < 4; ++r) det_exp_tab_s2(E[r]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) pr[r] = 1.0 / (1.0 + det_exp_tab_fin(E[r]));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) det_log_tab_s1((y[r] >= 0.5) ? pr[r] : 1.0 - pr[r], Lg[r], ltab);   // Y ~ Bernoulli
+#pragma unroll
+                for (int r = 0; r < 4; ++r) det_log_tab_s2(Lg[r]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    term[r] = det_log_tab_fin(Lg[r]);
+                    rv[r] = sgn * (y[r] - pr[r]);                                  // MCMCDerivRules.jl:111, closed form
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double resid = y[r] - eta[r];                            // resid = Y - X*vars
+                    const double zz = resid * isn;
+                    term[r] = -0.5 * (zz * zz + kLog2Pi) - logsn;                  // resid ~ Normal(0, sn)
+                    rv[r] = resid * is2n;
+                }
+            }
+            if (t < nfull) {                                                       // uniform: no padded observation
+#pragma unroll
+                for (int r = 0; r < 4; ++r) lik_part = lik_part + term[r];         // the lane's terms in (t, r) order
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool in = t * 16 + p.q + 4 * r < M.n;
+                    lik_part = in ? lik_part + term[r] : lik_part;
+                    rv[r] = in ? rv[r] : 0.0;
+                }
+            }
+            Rq[256 * (t & 1)] = f64x4{rv[0], rv[1], rv[2], rv[3]};
+            __syncthreads();
+        }
+    }
+    if (vwave) {
+        const double lik = glm_sum(a, p, GlmLds{}, lik_part);
+        if (p.q == 0) likl[p.tile * 16 + p.cl] = lik;
+    } else {
+        g_of(ntiles - 1);
+    }
+    __syncthreads();
+    if (vwave) return;
+    // ---- M waves: the end of the evaluation (glm_finish), MALA.jl:104-125
+    double lp = a.st.lp[cc];
+    int32_t n_acc = sa.tuner ? a.st.t_acc[cc] : 0;
+    int32_t n_prop = sa.tuner ? a.st.t_prop[cc] : 0;
+    if (sa.tuner) n_prop += 1;
+    const double qf = qfl[p.tile * 16 + p.cl];
+    bool oos;
+    double lpp;
+    {
+        const int d = M.d;
+        const double lik = likl[p.tile * 16 + p.cl];
+        const double sp = M.prior_sigma, s2p = sp * sp, logsp = det_log(sp);
+        double pp = 0.0;
+#pragma unroll
+        for (int slot = 0; slot < NS; ++slot) {
+            const int k = own_coord(p, slot);
+            if (k < d) {
+                const double z = (bx[slot] - 0.0) / sp;
+                pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
+            }
+        }
+        const double prior = glm_sum(a, p, GlmLds{}, pp);
+        double acc = 0.0 + prior;                                           // LLAcc(0.) + ...
+        bool bad = !(acc - acc == 0.0);
+        acc = acc + lik;
+        bad = bad || !(acc - acc == 0.0);
+        oos = bad;
+        if (bad) acc = -__builtin_inf();
+#pragma unroll
+        for (int slot = 0; slot < NS; ++slot)
+            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - bx[slot]) / s2p + G[slot >> 2][slot & 3];
+        lpp = acc;                                                          // MALA.jl:101
+    }
+    (void)oos;
+    double qb = 0.0;
+#pragma unroll
+    for (int slot = 0; slot < NS; ++slot) {
+        const bool v = glm_valid(a, p, slot);
+        const double xv = v ? xl[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
+        const double e = (bx[slot] + half * G[slot >> 2][slot & 3]) - xv;           // MALA.jl:104-105
+        if (v) qb = qb + ((-(e * e)) / twoh - Lc);
+    }
+    qb = glm_sum(a, p, GlmLds{}, qb);
+    const double ratio = ((lpp + qb) - lp) - qf;                   // MALA.jl:107
+    const bool acc = glm_mh_short_circuit(rs, chain, (uint32_t)i, ratio);
+    int64_t kk;
+    const bool kept = kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk);
+    double* const ks = kept && s.samples ? s.samples + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
+    double* const kg = kept && s.grads ? s.grads + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
+    if (p.live) {
+        double* const xw = a.st.x + (size_t)(4 * p.q) * ld + (size_t)p.c;
+        double* const gw = a.st.g + (size_t)(4 * p.q) * ld + (size_t)p.c;
+        const size_t Cs = (size_t)s.C;
+#pragma unroll
+        for (int slot = 0; slot < NS; ++slot) {
+            if (!glm_valid(a, p, slot)) continue;
+            const size_t r = (size_t)(16 * (slot >> 2) + (slot & 3));
+            double xv, gv;
+            if (acc) {
+                xv = bx[slot];
+                gv = G[slot >> 2][slot & 3];
+                xw[r * ld] = xv;
+                gw[r * ld] = gv;
+            } else {
+                xv = xl[r * ld];
+                gv = gl[r * ld];
+            }
+            const size_t ko = (size_t)(4 * p.q + r) * Cs + (size_t)p.c;
+            if (ks) ks[ko] = xv;
+            if (kg) kg[ko] = gv;
+        }
+    }
+    double hn = h;
+    if (acc) {
+        lp = lpp;
+        if (sa.tuner) n_acc += 1;
+    }
+    if (kept) glm_store_bit(a, p, kk, acc);
+    if (sa.tuner && i <= s.tuner_burnin && (i % sa.adapt_step) == 0) {   // MALA.jl:116-118
+        hn = h * glm_tune_factor(n_acc, n_prop, sa.target_rate);
+        n_acc = 0;
+        n_prop = 0;
+    }
+    if (p.live && p.q == 0) {
+        a.st.lp[p.c] = lp;
+        if (sa.tuner) {
+            a.st.t_step[p.c] = hn;
+            a.st.t_acc[p.c] = n_acc;
+            a.st.t_prop[p.c] = n_prop;
+        }
+    }
+    glm_count_evals(a, p, s.nsteps);
+}
+
 // storeLeaps: leap l's state into the record, [l][d][C] and [l][C] (HMC.jl:145-150)
 template <int NM>
 __device__ __forceinline__ void glm_rec_put(const GlmArgs& a, const GlmPos& p, int64_t l, const double (&x)[4 * NM],
@@ -1196,6 +1563,17 @@ static unsigned glm_grid(int64_t C, const GlmShape& g) {
 // glm_mala1.hip: the single-slice MALA kernels only, in a translation unit built with machine LICM
 hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
     using namespace mcmc;
+#if GLM_MALA1_WS
+    (void)lds;
+    const size_t lw = glm_ws_lds_doubles(a.g.nm, a.g.lds_stride) * sizeof(double);
+    switch (nm) {
+        case 1: glm_mala1ws<1><<<grid, 512, lw, st>>>(a); break;
+        case 2: glm_mala1ws<2><<<grid, 512, lw, st>>>(a); break;
+        case 4: glm_mala1ws<4><<<grid, 512, lw, st>>>(a); break;
+        case 8: glm_mala1ws<8><<<grid, 512, lw, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+#else
     constexpr int B = glm_block<1>();
     switch (nm) {
         case 1: glm_mala1<1><<<grid, B, lds, st>>>(a); break;
@@ -1204,6 +1582,7 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
         case 8: glm_mala1<8><<<grid, B, lds, st>>>(a); break;
         default: return hipErrorInvalidValue;
     }
+#endif
     return hipGetLastError();
 }
 #else
@@ -1250,7 +1629,7 @@ static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hip
     switch (a.sa.kind) {
         case SK_RWM: mcmc_note_step_kernel("glm_rwm<%d, %d>", NM, NW); break;
         case SK_MALA:
-            if (NW == 1) mcmc_note_step_kernel("glm_mala1<%d>", NM);
+            if (NW == 1) mcmc_note_step_kernel(GLM_MALA1_WS ? "glm_mala1ws<%d>" : "glm_mala1<%d>", NM);
             else mcmc_note_step_kernel("glm_mala<%d, %d>", NM, NW);
             break;
         case SK_HMC: mcmc_note_step_kernel("glm_hmc<%d, %d, false>", NM, NW); break;

@@ -177,3 +177,25 @@ def test_few_chain_rwm_models_and_sizes(gpu, C, d):
         _check(ch, s, acc)
         assert np.array_equal(ch.final_x, oc.x) and np.array_equal(ch.final_lp, oc.lp)
         assert ch.task.evals == C * 97
+
+
+@pytest.mark.parametrize("tuned", [False, True])
+@pytest.mark.parametrize("link_sign", [1.0, -1.0])
+def test_config3_logistic_mala_instance(gpu, tuned, link_sign):
+    """config 3's kernel: logistic regression n=1000, d=128 under MALA(0.001) (test/test_syntax.jl:28's sampler),
+    the wave-specialised glm_mala1ws<8> (M and V waves on one SIMD); 200 chains (a partial 64-chain workgroup),
+    bitwise against the oracle over several launches (one step per launch), tuned and untuned, both link signs."""
+    from test_gpu_parity import _glm_model
+    m0 = _glm_model("logistic", 128, n=1000)
+    X, Y = m0.target.X, m0.target.Y
+    m = mc.model(mc.LogisticRegression(X, Y, link_sign=link_sign), vars=np.zeros(128), gradient=True)
+    smp = (lambda: mc.MALA(0.001, mc.EmpMCTuner(0.6, adaptStep=2))) if tuned else (lambda: mc.MALA(0.001))
+    r = mc.SerialMC(steps=5, burnin=1, thinning=2)
+    t = (m * smp() * r).batch(200, seed=31)
+    chain = mc.run(t)
+    assert t.step_kernel == "glm_mala1ws<8>"
+    oc = orc.OracleChains(m, smp(), nchains=200, seed=31)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    _check(chain, s_ref, acc_ref)
+    assert np.array_equal(chain._gradients.view(np.uint64), g_ref.view(np.uint64)), "gradients not bit-identical"
+    assert np.array_equal(chain.final_lp, oc.lp)
