@@ -146,15 +146,32 @@ def measured_traffic(wkey, kname):
             "source": e["source"], "unit": "B"}
 
 
+def step_kernel_src_hash():
+    """sha256 over the sources the lane- and wave-per-chain step kernels are compiled from (csrc/*.hpp, the
+    Box-Muller tables, kernels/lpc*, kernels/wpc*): a VALU profile recorded under another hash measured other code."""
+    import glob
+    import hashlib
+    base = os.path.join(ROOT, "mcmc.jl_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(base, "*.hpp")) + glob.glob(os.path.join(base, "*.inc"))
+                   + glob.glob(os.path.join(base, "kernels", "lpc*")) + glob.glob(os.path.join(base, "kernels", "wpc*"))
+                   + [os.path.join(base, "kernels", "layout_api.hpp")])
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, base).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def measured_valu(kname):
     """VALU issue cost of the step kernel per chain-step (SQ_ACTIVE_INST_VALU quad-cycles / chain-steps of the
     timed dispatch) and its measured VALU-busy fraction, from a committed rocprofv3 PMC run of this kernel
-    instance (profiles/valu.json, written by scripts/summarize_valu.py), or None."""
+    instance built from these sources (profiles/valu.json, written by scripts/summarize_valu.py), or None."""
     p = os.path.join(ROOT, "profiles", "valu.json")
     if not os.path.exists(p):
         return None
+    h = step_kernel_src_hash()
     for k, e in json.load(open(p)).items():
-        if _norm_kernel(k) == _norm_kernel(kname):
+        if _norm_kernel(k) == _norm_kernel(kname) and e.get("src_hash") == h:
             return e
     return None
 
@@ -447,7 +464,8 @@ def main():
                     "launches": launches, "avg_launch_ms": avg_launch_s * 1e3,
                     "algorithmic_bytes_per_launch": fused / launches, "units_per_launch": units,
                     "survey_bytes": survey_bytes,
-                    "note": "no committed VALU profile of this kernel instance: HBM roofline of the fused design"}
+                    "note": "no committed VALU profile of this kernel instance built from these sources "
+                            "(profiles/valu.json src_hash): HBM roofline of the fused design"}
     else:
         flop_per_eval = 4.0 * cfg0["n"] * d                           # eta = X beta, then X^T r
         flops = flop_per_eval * evals

@@ -215,31 +215,30 @@ __device__ __forceinline__ void det_sincos2pi(double u, double& s_out, double& c
 
 // log((w + 0.5) 2^-32) for the Box-Muller radius: table-driven (bm_log_table.inc), division- and
 // branch-free, no special cases (the argument is always in [2^-33, 1)).  x = w + 0.5 = 2^e m, the
-// top 7 mantissa bits select c (c = 1 for the intervals next to 1, so results near 0 keep full
-// relative precision); r = m' inv_c - 1 with |r| < 2^-7; log = e ln2 + T + log1p(r), log1p by a
-// degree-8 Horner polynomial.
+// top 9 mantissa bits select c (c = 1 for the intervals next to 1, so results near 0 keep full
+// relative precision); r = m' inv_c - 1 with |r| < 2^-9; log = e ln2 + T + log1p(r), log1p by a
+// degree-6 Horner polynomial (truncation r^7/7 < 2^-54 |r|).  Round 2: 512 rows and degree 6 in place of 128
+// rows and degree 8 (two fmas fewer per normal pair).  kBmLogTab (128 rows) stays for det_log_tab.
 static __device__ const double kBmLogTab[128][4] = {BM_LOG_TABLE_ROWS};
+static __device__ const double kBmLog512Tab[512][4] = {BM_LOG512_TABLE_ROWS};
 
-__device__ __forceinline__ double bm_log_u32(uint32_t w, const double (*tab)[4] = kBmLogTab) {
+__device__ __forceinline__ double bm_log_u32(uint32_t w, const double (*tab)[4] = kBmLog512Tab) {
     const double ln2_hi = 0x1.62e42fee00000p-1;
     const double ln2_lo = 0x1.a39ef35793c76p-33;
     const double x = (double)w + 0.5;                                   // exact
     const uint64_t b = d2bits(x);
-    // all on the high word xh (x > 0): top7 = xh[19:13], up = xh[19] (m in [1.5, 2): use m/2), e from xh[30:20];
-    // m's high word is xh's mantissa bits under exponent 0x3ff - up = 0x3ff ^ up.  Three integer operations
-    // fewer than the 64-bit form, the same values.
+    // all on the high word xh (x > 0): top9 = xh[19:11], up = xh[19] (m in [1.5, 2): use m/2), e from xh[30:20];
+    // m's high word is xh's mantissa bits under exponent 0x3ff - up = 0x3ff ^ up
     const uint32_t xh = (uint32_t)(b >> 32);
     const uint32_t up = (xh >> 19) & 1u;
     const int e = (int)(xh >> 20) + (int)up - (1023 + 32);
     const uint32_t mhi = ((0x3ffu ^ up) << 20) | (xh & 0x000fffffu);
     const double m = bits2d(((uint64_t)mhi << 32) | (b & 0xffffffffull));
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    const f64x2_t* row = reinterpret_cast<const f64x2_t*>(reinterpret_cast<const char*>(tab) + ((xh >> 8) & 0xfe0u));
+    const f64x2_t* row = reinterpret_cast<const f64x2_t*>(reinterpret_cast<const char*>(tab) + ((xh >> 6) & 0x3fe0u));
     const f64x2_t a = row[0], t = row[1];                               // (inv_c, T_hi), (T_lo, 0)
     const double r = __builtin_fma(m, a.x, -1.0);
-    double P = __builtin_fma(r, -0x1p-3, 0x1.2492492492492p-3);         // -1/8, 1/7
-    P = __builtin_fma(r, P, -0x1.5555555555555p-3);                     // -1/6
-    P = __builtin_fma(r, P, 0x1.999999999999ap-3);                      // 1/5
+    double P = __builtin_fma(r, -0x1.5555555555555p-3, 0x1.999999999999ap-3);   // -1/6, 1/5
     P = __builtin_fma(r, P, -0x1p-2);                                   // -1/4
     P = __builtin_fma(r, P, 0x1.5555555555555p-2);                      // 1/3
     P = __builtin_fma(r, P, -0x1p-1);                                   // -1/2
@@ -368,26 +367,22 @@ __device__ __forceinline__ double det_log_tab(double v, const double (*tab)[4] =
     return det_log_tab_fin(L);
 }
 
-// sin, cos of 2 pi w 2^-32 (the Box-Muller angle), table-driven: the angle splits as k/256 + j 2^-32 turns
-// with k = (w + 2^23) >> 24 and |j| <= 2^23, so r = 2 pi j 2^-32 has |r| <= 2 pi 2^-9.  The row of k gives
-// (sin a, cos a) (scripts/gen_bm_log_table.py, full circle: no quadrant selects); sin r and cos r - 1 by
-// Taylor polynomials (truncation < 2^-66 relative); sin(a+r) = sa + (ca sin r + sa (cos r - 1)).
-static __device__ const double kBmSinCosTab[256][2] = {BM_SINCOS_TABLE_ROWS};
+// sin, cos of 2 pi w 2^-32 (the Box-Muller angle), table-driven: the angle splits as k/1024 + j 2^-32 turns
+// with k = (w + 2^21) >> 22 and |j| <= 2^21, so r = 2 pi j 2^-32 has |r| <= 2 pi 2^-11.  The row of k gives
+// (sin a, cos a) (scripts/gen_bm_log_table.py, full circle: no quadrant selects); sin r = r - r^3/6 + r^5/120
+// (truncation r^7/5040 < 2^-70) and cos r - 1 = -r^2/2 + r^4/24 (truncation r^6/720 < 2^-59);
+// sin(a+r) = sa + (ca sin r + sa (cos r - 1)).  Round 2: 1024 rows in place of 256 (one fma fewer in each series).
+static __device__ const double kBmSinCos1024Tab[1024][2] = {BM_SINCOS1024_TABLE_ROWS};
 
 __device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, double& c_out,
-                                                  const double (*sct)[2] = kBmSinCosTab) {
-    const uint32_t t = w + 0x800000u;
-    const uint32_t k = t >> 24;
-    // j = (t & 0xffffff) - 2^23 is the sign-extended low 24 bits of w (checked for all 2^32 w): one v_bfe_i32.
-    // (Written as shifts: __builtin_amdgcn_sbfe here was followed by an unsigned int-to-double conversion.)
-    const double r = (double)(((int32_t)(w << 8)) >> 8) * 0x1.921fb54442d18p-30;
+                                                  const double (*sct)[2] = kBmSinCos1024Tab) {
+    const uint32_t k = (w + 0x200000u) >> 22;
+    // j = the sign-extended low 22 bits of w (w - 2^22 k), one v_bfe_i32
+    const double r = (double)(((int32_t)(w << 10)) >> 10) * 0x1.921fb54442d18p-30;
     const double r2 = r * r;
-    double sp = __builtin_fma(r2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);   // -1/5040, 1/120
-    sp = __builtin_fma(r2, sp, -0x1.5555555555555p-3);                             // -1/6
+    const double sp = __builtin_fma(r2, 0x1.1111111111111p-7, -0x1.5555555555555p-3);   // 1/120, -1/6
     const double sr = __builtin_fma(r * r2, sp, r);
-    double cp = __builtin_fma(r2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);   // -1/720, 1/24
-    cp = __builtin_fma(r2, cp, -0.5);
-    const double cm1 = r2 * cp;
+    const double cm1 = r2 * __builtin_fma(r2, 0x1.5555555555555p-5, -0.5);                // 1/24, -1/2
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
     const f64x2_t a = *reinterpret_cast<const f64x2_t*>(sct[k]);                   // (sin a, cos a)
     s_out = a.x + __builtin_fma(a.y, sr, a.x * cm1);
@@ -416,8 +411,8 @@ __device__ __forceinline__ double sqrt_pos_normal(double x) {
 // angle 2 pi u2, u2 = w.y 2^-32.
 // tab, sct: the radius-log and angle tables, in global memory (default) or a kernel's LDS copies
 __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3,
-                                         const double (*tab)[4] = kBmLogTab,
-                                         const double (*sct)[2] = kBmSinCosTab) {
+                                         const double (*tab)[4] = kBmLog512Tab,
+                                         const double (*sct)[2] = kBmSinCos1024Tab) {
     {
         const double rad = sqrt_pos_normal(-2.0 * bm_log_u32(w.x, tab));
         double s, c;
@@ -430,6 +425,21 @@ __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1,
         det_sincos2pi_u32(w.w, s, c, sct);
         z2 = rad * c; z3 = rad * s;
     }
+}
+
+// ratio > det_log(u), exactly (the RWM / MALA test `ratio > log(rand())`, RWM.jl:63, MALA.jl:108).  A
+// single-precision log2 (v_log_f32) decides it when ratio is not within E = 2^-16 (1 + |L|) of L = log2f(u) ln2:
+// |L - log u| <= ln2 (2^-23 |log2 u| + 2^-24 log2 e) plus the 1-ulp error of det_log is hundreds of times smaller
+// than E, so a decided test agrees with the exact one.  The rest (probability ~1e-5 per test; u = 0; NaN ratios)
+// takes det_log, on the lanes that need it.
+__device__ __forceinline__ bool gt_det_log(double ratio, double u) {
+    const double L = (double)__builtin_amdgcn_logf((float)u) * 0x1.62e42fefa39efp-1;
+    const double E = 0x1p-16 * (1.0 + __builtin_fabs(L));
+    const bool sure_acc = ratio > L + E;
+    const bool sure_rej = ratio <= L - E;
+    bool acc = sure_acc;
+    if (!sure_acc && !sure_rej) acc = ratio > det_log(u);
+    return acc;
 }
 
 __device__ __forceinline__ double round_away(double x) {

@@ -637,7 +637,7 @@ __device__ __forceinline__ bool glm_mh_short_circuit(const Stream& rs, uint32_t 
     bool acc = ratio > 0.0;                                           // RWM.jl:63, MALA.jl:108
     if (!acc) {
         const u32x4 w = rs.block(chain, step, 0u, TAG_ACCEPT);
-        acc = ratio > det_log(uniform53(w.x, w.y));
+        acc = gt_det_log(ratio, uniform53(w.x, w.y));
     }
     return acc;
 }

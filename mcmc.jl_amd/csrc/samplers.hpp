@@ -33,6 +33,35 @@ namespace mcmc {
 
 constexpr int kBlock = 256;
 
+// The Box-Muller tables (32 KB) into a block's LDS: every 16-byte load in flight before the first store (a loop
+// of load-store pairs costs one L2 round trip per iteration), then one barrier.  kBlock threads.
+__device__ __forceinline__ void stage_bm_tables(double (*lt)[4], double (*ls)[2]) {
+    typedef double f64x2_t __attribute__((ext_vector_type(2)));
+    constexpr int kN = 1024 / kBlock;                       // 16-byte rows per thread per table
+    const f64x2_t* gt = reinterpret_cast<const f64x2_t*>(&kBmLog512Tab[0][0]);
+    const f64x2_t* gs = reinterpret_cast<const f64x2_t*>(&kBmSinCos1024Tab[0][0]);
+    f64x2_t a[kN], b[kN];
+#pragma unroll
+    for (int j = 0; j < kN; ++j) {
+        a[j] = gt[threadIdx.x + kBlock * j];
+        b[j] = gs[threadIdx.x + kBlock * j];
+    }
+#pragma unroll
+    for (int j = 0; j < kN; ++j) {
+        reinterpret_cast<f64x2_t*>(&lt[0][0])[threadIdx.x + kBlock * j] = a[j];
+        reinterpret_cast<f64x2_t*>(&ls[0][0])[threadIdx.x + kBlock * j] = b[j];
+    }
+    __syncthreads();
+}
+
+// The block's LDS copies of the Box-Muller tables (one allocation per kernel, whoever asks)
+__device__ __forceinline__ void bm_lds_tables(const double (*&lt)[4], const double (*&ls)[2]) {
+    __shared__ __attribute__((aligned(16))) double lds_tab[512][4];
+    __shared__ __attribute__((aligned(16))) double lds_sct[1024][2];
+    lt = lds_tab;
+    ls = lds_sct;
+}
+
 // ------------------------------------------------------------------ mappings
 // NB = ceil(d/4).  FULL: d == 4 NB, every register coordinate is a real one -- no validity masks
 // (with a runtime d they are per-coordinate uniform masks, which overflow the SGPR file at NB = 8).
@@ -45,20 +74,15 @@ struct LaneChain {
     int d;
     const double (*tab)[4];   // LDS copies of the Box-Muller log and angle tables: per-lane row gathers
     const double (*sct)[2];   // from LDS, not from the vector L1 (every block thread calls the constructor)
-    __device__ LaneChain(const StepArgs& s) {
+    // defer: the caller issues its state loads first and then calls stage() (the two latencies overlap)
+    __device__ LaneChain(const StepArgs& s, bool defer = false) {
         c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
         live = c < s.C;
         d = s.d;
-        __shared__ __attribute__((aligned(16))) double lds_tab[128][4];
-        __shared__ __attribute__((aligned(16))) double lds_sct[256][2];
-        for (int i = threadIdx.x; i < 128 * 4; i += kBlock) {
-            lds_tab[i >> 2][i & 3] = kBmLogTab[i >> 2][i & 3];
-            lds_sct[i >> 1][i & 1] = kBmSinCosTab[i >> 1][i & 1];
-        }
-        __syncthreads();
-        tab = lds_tab;
-        sct = lds_sct;
+        bm_lds_tables(tab, sct);
+        if (!defer) stage();
     }
+    __device__ __forceinline__ void stage() const { stage_bm_tables(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct)); }
     __device__ __forceinline__ int coord(int k) const { return k; }
     // blocks 0..NB-2 are always full (NB = ceil(d/4)); only the last block's coordinates are tested
     __device__ __forceinline__ bool valid(int k) const { return FULL || k < 4 * (NB - 1) || k < d; }
@@ -149,22 +173,16 @@ struct WaveChain {
     int64_t ldr;      // row stride of chain-major state (multiple of 4)
     const double (*tab)[4];   // LDS copies of the Box-Muller tables (as LaneChain)
     const double (*sct)[2];
-    __device__ WaveChain(const StepArgs& s) {
+    __device__ WaveChain(const StepArgs& s, bool defer = false) {
         c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
         live = c < s.C;
         d = s.d;
         lane = threadIdx.x & 63;
         ldr = s.ld;
-        __shared__ __attribute__((aligned(16))) double lds_tab[128][4];
-        __shared__ __attribute__((aligned(16))) double lds_sct[256][2];
-        for (int i = threadIdx.x; i < 128 * 4; i += kBlock) {
-            lds_tab[i >> 2][i & 3] = kBmLogTab[i >> 2][i & 3];
-            lds_sct[i >> 1][i & 1] = kBmSinCosTab[i >> 1][i & 1];
-        }
-        __syncthreads();
-        tab = lds_tab;
-        sct = lds_sct;
+        bm_lds_tables(tab, sct);
+        if (!defer) stage();
     }
+    __device__ __forceinline__ void stage() const { stage_bm_tables(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct)); }
     __device__ __forceinline__ int coord(int k) const { return 4 * (lane + 64 * (k >> 2)) + (k & 3); }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + 64 * b); }
@@ -268,7 +286,7 @@ __device__ __forceinline__ bool mh_accept_short_circuit(const Stream& rs, uint32
     bool acc = ratio > 0.0;
     if (!acc) {
         const u32x4 w = rs.block(chain, step, 0u, TAG_ACCEPT);
-        acc = ratio > det_log(uniform53(w.x, w.y));
+        acc = gt_det_log(ratio, uniform53(w.x, w.y));
     }
     return acc;
 }
@@ -284,15 +302,16 @@ __device__ __forceinline__ double tune_factor(int32_t acc, int32_t prop, double 
 template <class P, class M, bool US = false>
 __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     const StepArgs& s = a.s;
-    const P p(s);
+    const P p(s, true);
     const M model(a.m);
     const Stream rs{s.key0, s.key1};
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
     double x[P::NC], sc[P::NC];
-    p.load(a.st.x, s.ld, x);
+    p.load(a.st.x, s.ld, x);                                    // in flight while the tables are staged
+    double lp = p.load_scalar(a.st.lp);
+    p.stage();
 #pragma unroll
     for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
-    double lp = p.load_scalar(a.st.lp);
 
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;

@@ -16,7 +16,7 @@
  *                       path, explicit fma in the polynomial
  *   det_exp ........... Cody-Waite reduction + degree-13 Taylor (fma Horner)
  *   det_sincos2pi ..... exact quarter-turn reduction + Taylor polynomials in r
- *   Box-Muller angle .. 256-row sin/cos table + short Taylor polynomials (orc_sincos2pi_u32)
+ *   Box-Muller angle .. 1024-row sin/cos table + short Taylor polynomials (orc_sincos2pi_u32)
  *   Box-Muller ........ normals from 32-bit uniforms, 4 normals per Philox block
  *
  * Compile with -ffp-contract=off: every fused multiply-add is an explicit fma();
@@ -185,12 +185,13 @@ static inline void orc_sincos2pi(double u, double* s_out, double* c_out) {
 }
 
 /* ------------------------------------------------------- Box-Muller radius logarithm */
-/* log((w + 0.5) 2^-32), w a 32-bit draw: x = w + 0.5 = 2^e m (exact); the top 7 mantissa bits pick
-   the table row (scripts/gen_bm_log_table.py): for m >= 1.5 the reduction uses m/2 and e+1, and the
-   rows next to 1 have c = 1, so a result near 0 keeps its relative precision.  r = m' inv_c - 1
-   (|r| < 2^-7), log = e ln2 + (T_hi + T_lo) + log1p(r), log1p by Horner to degree 8.  The device
-   twin is bm_log_u32 (csrc/detmath.hpp). */
+/* log((w + 0.5) 2^-32), w a 32-bit draw: x = w + 0.5 = 2^e m (exact); the top 9 mantissa bits pick
+   the table row (scripts/gen_bm_log_table.py, BM_LOG512_TABLE_ROWS): for m >= 1.5 the reduction uses m/2 and
+   e+1, and the rows next to 1 have c = 1, so a result near 0 keeps its relative precision.  r = m' inv_c - 1
+   (|r| < 2^-9), log = e ln2 + (T_hi + T_lo) + log1p(r), log1p by Horner to degree 6.  The device twin is
+   bm_log_u32 (csrc/detmath.hpp).  The 128-row table (top 7 bits, degree 8) stays for orc_log_tab. */
 static const double orc_bm_log_tab[128][4] = {BM_LOG_TABLE_ROWS};
+static const double orc_bm_log512_tab[512][4] = {BM_LOG512_TABLE_ROWS};
 
 static inline double orc_bm_log_u32(uint32_t w) {
     const double ln2_hi = 0x1.62e42fee00000p-1;
@@ -198,17 +199,15 @@ static inline double orc_bm_log_u32(uint32_t w) {
     double x = (double)w + 0.5;
     uint64_t b;
     memcpy(&b, &x, 8);
-    uint32_t top7 = (uint32_t)(b >> 45) & 0x7fu;
-    uint32_t up = top7 >> 6;
+    uint32_t top9 = (uint32_t)(b >> 43) & 0x1ffu;
+    uint32_t up = top9 >> 8;
     int e = (int)(uint32_t)(b >> 52) - 1023 + (int)up - 32;
     uint64_t mb = (b & 0x000fffffffffffffull) | ((uint64_t)(0x3ffu - up) << 52);
     double m;
     memcpy(&m, &mb, 8);
-    const double* row = orc_bm_log_tab[top7];
+    const double* row = orc_bm_log512_tab[top9];
     double r = fma(m, row[0], -1.0);
-    double P = fma(r, -0x1p-3, 0x1.2492492492492p-3);
-    P = fma(r, P, -0x1.5555555555555p-3);
-    P = fma(r, P, 0x1.999999999999ap-3);
+    double P = fma(r, -0x1.5555555555555p-3, 0x1.999999999999ap-3);
     P = fma(r, P, -0x1p-2);
     P = fma(r, P, 0x1.5555555555555p-2);
     P = fma(r, P, -0x1p-1);
@@ -279,24 +278,21 @@ static inline double orc_log_tab(double v) {
 }
 
 /* ------------------------------------------------------- Box-Muller angle */
-/* sin, cos of 2 pi w 2^-32: angle = k/256 + j 2^-32 turns, k = (w + 2^23) >> 24, |j| <= 2^23; the row of k
-   holds RN(sin, cos of 2 pi k/256) (scripts/gen_bm_log_table.py); r = 2 pi j 2^-32 (|r| <= 2 pi 2^-9),
-   sin r and cos r - 1 by Taylor (truncation < 2^-66 relative), then the angle-addition formula.  The
-   device twin is det_sincos2pi_u32 (csrc/detmath.hpp). */
-static const double orc_bm_sincos_tab[256][2] = {BM_SINCOS_TABLE_ROWS};
+/* sin, cos of 2 pi w 2^-32: angle = k/1024 + j 2^-32 turns, k = (w + 2^21) >> 22, |j| <= 2^21; the row of k
+   holds RN(sin, cos of 2 pi k/1024) (scripts/gen_bm_log_table.py, BM_SINCOS1024_TABLE_ROWS); r = 2 pi j 2^-32
+   (|r| <= 2 pi 2^-11), sin r to r^5 and cos r - 1 to r^4 (truncation < 2^-59), then the angle-addition
+   formula.  The device twin is det_sincos2pi_u32 (csrc/detmath.hpp). */
+static const double orc_bm_sincos1024_tab[1024][2] = {BM_SINCOS1024_TABLE_ROWS};
 
 static inline void orc_sincos2pi_u32(uint32_t w, double* s_out, double* c_out) {
-    uint32_t t = w + 0x800000u;
-    uint32_t k = t >> 24;
-    double r = (double)((int32_t)(t & 0xffffffu) - 0x800000) * 0x1.921fb54442d18p-30;
+    uint32_t t = w + 0x200000u;
+    uint32_t k = t >> 22;
+    double r = (double)((int32_t)(t & 0x3fffffu) - 0x200000) * 0x1.921fb54442d18p-30;
     double r2 = r * r;
-    double sp = fma(r2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);
-    sp = fma(r2, sp, -0x1.5555555555555p-3);
+    double sp = fma(r2, 0x1.1111111111111p-7, -0x1.5555555555555p-3);
     double sr = fma(r * r2, sp, r);
-    double cp = fma(r2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);
-    cp = fma(r2, cp, -0.5);
-    double cm1 = r2 * cp;
-    double sa = orc_bm_sincos_tab[k][0], ca = orc_bm_sincos_tab[k][1];
+    double cm1 = r2 * fma(r2, 0x1.5555555555555p-5, -0.5);
+    double sa = orc_bm_sincos1024_tab[k][0], ca = orc_bm_sincos1024_tab[k][1];
     *s_out = sa + fma(ca, sr, sa * cm1);
     *c_out = ca + fma(-sa, sr, ca * cm1);
 }

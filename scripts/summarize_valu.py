@@ -71,6 +71,9 @@ L = [f"# VALU roofline: {tag}", "", f"kernel: `{kname}`", f"workload: `{bl['conf
 for c in sorted(v):
     L.append(f"| {c} | {v[c]:.6g} | {v[c] / waves / steps:.2f} |")
 open(os.path.join(root, "profiles", f"{tag}.md"), "w").write("\n".join(L) + "\n")
+sys.path.insert(0, root)
+from bench import step_kernel_src_hash  # noqa: E402
+entry["src_hash"] = step_kernel_src_hash()   # the sources this profile measured (bench.py ignores other hashes)
 p = os.path.join(root, "profiles", "valu.json")
 tj = json.load(open(p)) if os.path.exists(p) else {}
 tj[kname] = entry
