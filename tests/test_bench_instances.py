@@ -199,3 +199,20 @@ def test_config3_logistic_mala_instance(gpu, tuned, link_sign):
     _check(chain, s_ref, acc_ref)
     assert np.array_equal(chain._gradients.view(np.uint64), g_ref.view(np.uint64)), "gradients not bit-identical"
     assert np.array_equal(chain.final_lp, oc.lp)
+
+
+@pytest.mark.parametrize("d,scale,spl", [(2, 1.5, 0), (4, 1.5, 0), (3, 0.1, 0), (3, 0.6, 700), (1, 3.0, 999)])
+def test_speculation_long_and_rejecting(gpu, d, scale, spl):
+    """lpc_rwm_spec (one chain, d <= 4): 2 500 steps (13 stage halves of pre-drawn increments), at acceptance rates
+    from ~96 % down to ~10 %, over one launch or launches of 700 / 999 steps (blocks cut by launch boundaries);
+    thinning 3 with a burnin that ends inside a 6-step block."""
+    m = mc.model(mc.IsoNormalDot(), init=np.linspace(0.5, 1.0, d))
+    r = mc.SerialMC(steps=2500, burnin=37, thinning=3)
+    t = (m * mc.RWM(scale) * r).batch(1, seed=11, steps_per_launch=spl)
+    ch = mc.run(t)
+    assert t.step_kernel.startswith("lpc_rwm_spec")
+    oc = orc.OracleChains(m, mc.RWM(scale), nchains=1, seed=11)
+    s, _, acc = oc.run(r)
+    _check(ch, s, acc)
+    assert np.array_equal(ch.final_x, oc.x) and np.array_equal(ch.final_lp, oc.lp)
+    assert t.evals == 2500

@@ -90,6 +90,25 @@ def test_device_detmath_bitwise(gpu, op, name):
     assert same.all(), f"{name}: {np.count_nonzero(~same)} mismatches, e.g. x={x[~same][:3]}"
 
 
+def test_screened_accept_test_is_exact(gpu):
+    """gt_det_log (the RWM/MALA test ratio > log(rand()), RWM.jl:63, screened by an f32 log2) against the oracle's
+    ratio > det_log(u): ratios at det_log(u) itself, one ulp either side, inside and just outside the screen's
+    band E = 2^-16 (1 + |L|), far away, and the special values (u = 0 -> -inf; NaN, +-inf ratios; u near 1)."""
+    rng = np.random.default_rng(15)
+    u = np.concatenate([rng.uniform(0, 1, 20000), 1 - np.exp(rng.uniform(-36, -1, 5000)), np.exp(rng.uniform(-36, 0, 5000)),
+                        [0.0, 2.0**-53, 1 - 2.0**-53, 0.5]])
+    L = orc.detmath(0, u)
+    E = 2.0**-16 * (1 + np.abs(np.where(np.isfinite(L), L, 0)))
+    ratios = [L, np.nextafter(L, np.inf), np.nextafter(L, -np.inf), L + 0.3 * E, L - 0.3 * E, L + 0.999 * E,
+              L - 0.999 * E, L + 3 * E, L - 3 * E, L + 1.0, L - 1.0, np.zeros_like(u), np.full_like(u, np.nan),
+              np.full_like(u, -np.inf), np.full_like(u, np.inf)]
+    r = np.concatenate(ratios)
+    uu = np.tile(u, len(ratios))
+    d, h = _dev_math(15, r, uu), orc.detmath(15, r, uu)
+    assert np.array_equal(d, h), f"{np.count_nonzero(d != h)} decisions differ"
+    assert 0 < h.mean() < 1
+
+
 def test_device_normals_bitwise(gpu):
     n = 50000
     a = np.arange(n, dtype=float) + 2.0**32 * 3
