@@ -502,7 +502,7 @@ extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, 
     mcmc_ctx* ctx = m->ctx;
     if (int r = set_device(ctx)) return r;
     const int d = m->args.d;
-    if (model_is_separable(m) && d > mcmc_wpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "d > 2048 is not built");
+    if (model_is_separable(m) && d > mcmc_wpc_max_d()) return fail(MCMC_E_UNSUPPORTED, "d > 16384 is not built");
     const Layout L = layout_for(m);
     const int64_t ld = ld_for(L, nchains, d);
     const size_t nst = L != LAYOUT_WPC ? (size_t)d * ld : (size_t)nchains * ld;
@@ -610,7 +610,7 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (int r = set_device(ctx)) return r;
     const int d = m->args.d;
     if (model_is_separable(m) && d > mcmc_wpc_max_d())
-        return fail(MCMC_E_UNSUPPORTED, "separable targets support d <= 2048");
+        return fail(MCMC_E_UNSUPPORTED, "separable targets support d <= 16384");
     auto* c = new mcmc_chains();
     c->model = m;
     m->chains_alive += 1;

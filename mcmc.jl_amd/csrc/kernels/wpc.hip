@@ -1,10 +1,10 @@
-// wpc.hip -- dispatch of the wave-per-chain kernels (32 < d <= 2048) on the model kind; the kernels
+// wpc.hip -- dispatch of the wave- and block-per-chain kernels (32 < d <= 16384) on the model kind; the kernels
 // live in wpc_impl.hpp, instantiated per model by wpc_<model>.hip.
 #include "layout_api.hpp"
 
 hipError_t mcmc_launch_wpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
     using namespace mcmc;
-    if (a.s.d < 1 || a.s.d > 2048) return hipErrorInvalidValue;
+    if (a.s.d < 1 || a.s.d > 16384) return hipErrorInvalidValue;
     switch (a.m.kind) {
         case MK_ISO: return mcmc_wpc_step_iso(a, st);
         case MK_NORMAL: return mcmc_wpc_step_normal(a, st);
@@ -17,7 +17,7 @@ hipError_t mcmc_launch_wpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
 hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st) {
     using namespace mcmc;
-    if (a.s.d < 1 || a.s.d > 2048) return hipErrorInvalidValue;
+    if (a.s.d < 1 || a.s.d > 16384) return hipErrorInvalidValue;
     switch (a.m.kind) {
         case MK_ISO: return mcmc_wpc_eval_iso(a, xin, lp, g, check, st);
         case MK_NORMAL: return mcmc_wpc_eval_normal(a, xin, lp, g, check, st);
@@ -29,7 +29,7 @@ hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, do
 
 hipError_t mcmc_launch_wpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec& r, hipStream_t st) {
     using namespace mcmc;
-    if (a.s.d < 1 || a.s.d > 2048) return hipErrorInvalidValue;
+    if (a.s.d < 1 || a.s.d > 16384) return hipErrorInvalidValue;
     switch (a.m.kind) {
         case MK_ISO: return mcmc_wpc_record_iso(a, r, st);
         case MK_NORMAL: return mcmc_wpc_record_normal(a, r, st);
@@ -39,4 +39,4 @@ hipError_t mcmc_launch_wpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec
     }
 }
 
-int mcmc_wpc_max_d() { return 2048; }
+int mcmc_wpc_max_d() { return 16384; }

@@ -34,22 +34,24 @@ namespace mcmc {
 constexpr int kBlock = 256;
 
 // The Box-Muller tables (32 KB) into a block's LDS: every 16-byte load in flight before the first store (a loop
-// of load-store pairs costs one L2 round trip per iteration), then one barrier.  kBlock threads.
+// of load-store pairs costs one L2 round trip per iteration), then one barrier.  NT threads (kBlock, or the
+// block-per-chain kernels' 64 W).
+template <int NT = kBlock>
 __device__ __forceinline__ void stage_bm_tables(double (*lt)[4], double (*ls)[2]) {
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    constexpr int kN = 1024 / kBlock;                       // 16-byte rows per thread per table
+    constexpr int kN = 1024 / NT;                           // 16-byte rows per thread per table
     const f64x2_t* gt = reinterpret_cast<const f64x2_t*>(&kBmLog512Tab[0][0]);
     const f64x2_t* gs = reinterpret_cast<const f64x2_t*>(&kBmSinCos1024Tab[0][0]);
     f64x2_t a[kN], b[kN];
 #pragma unroll
     for (int j = 0; j < kN; ++j) {
-        a[j] = gt[threadIdx.x + kBlock * j];
-        b[j] = gs[threadIdx.x + kBlock * j];
+        a[j] = gt[threadIdx.x + NT * j];
+        b[j] = gs[threadIdx.x + NT * j];
     }
 #pragma unroll
     for (int j = 0; j < kN; ++j) {
-        reinterpret_cast<f64x2_t*>(&lt[0][0])[threadIdx.x + kBlock * j] = a[j];
-        reinterpret_cast<f64x2_t*>(&ls[0][0])[threadIdx.x + kBlock * j] = b[j];
+        reinterpret_cast<f64x2_t*>(&lt[0][0])[threadIdx.x + NT * j] = a[j];
+        reinterpret_cast<f64x2_t*>(&ls[0][0])[threadIdx.x + NT * j] = b[j];
     }
     __syncthreads();
 }
@@ -160,12 +162,31 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// FULL: d == 256 G, every lane coordinate is a real one -- no per-coordinate validity masks (with a
+// Sum of a per-chain quantity over the W waves of a block-per-chain kernel: each wave's butterfly, then the wave
+// sums left to right (oracle order W); two barriers (the partials buffer is reused by the next call)
+template <int W>
+__device__ __forceinline__ double block_sum(double v) {
+    v = wave_sum(v);
+    if (W == 1) return v;
+    __shared__ double part[W];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = part[0];
+#pragma unroll
+    for (int w = 1; w < W; ++w) t = t + part[w];
+    __syncthreads();
+    return t;
+}
+
+// FULL: d == 256 G W, every lane coordinate is a real one -- no per-coordinate validity masks (with a
 // runtime d they are 4 G lane masks live across the step loop, which spill the scalar file)
-template <int G, bool FULL = false>
+// W > 1: one chain per block of W waves (d up to 256 G W; kernels/wpc_impl.hpp bpc_*): lane l of the 64 W owns
+// coordinates 4 (l + 64 W k) + e, sums per lane, per wave, then over the waves (block_sum, oracle order W)
+template <int G, bool FULL = false, int W = 1>
 struct WaveChain {
     static constexpr int NB = G;
     static constexpr int NC = 4 * G;
+    static constexpr int L = 64 * W;                    // lanes per chain
     int64_t c;
     bool live;
     int d;
@@ -174,25 +195,27 @@ struct WaveChain {
     const double (*tab)[4];   // LDS copies of the Box-Muller tables (as LaneChain)
     const double (*sct)[2];
     __device__ WaveChain(const StepArgs& s, bool defer = false) {
-        c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        c = W == 1 ? (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
         live = c < s.C;
         d = s.d;
-        lane = threadIdx.x & 63;
+        lane = W == 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
         ldr = s.ld;
         bm_lds_tables(tab, sct);
         if (!defer) stage();
     }
-    __device__ __forceinline__ void stage() const { stage_bm_tables(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct)); }
-    __device__ __forceinline__ int coord(int k) const { return 4 * (lane + 64 * (k >> 2)) + (k & 3); }
+    __device__ __forceinline__ void stage() const {
+        stage_bm_tables<W == 1 ? kBlock : L>(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct));
+    }
+    __device__ __forceinline__ int coord(int k) const { return 4 * (lane + L * (k >> 2)) + (k & 3); }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
-    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + 64 * b); }
-    __device__ __forceinline__ double reduce(double v) const { return wave_sum(v); }
-    __device__ __forceinline__ bool any(bool v) const { return __ballot(v) != 0; }
+    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + L * b); }
+    __device__ __forceinline__ double reduce(double v) const { return block_sum<W>(v); }
+    __device__ __forceinline__ bool any(bool v) const { return W == 1 ? __ballot(v) != 0 : __syncthreads_or(v) != 0; }
     __device__ __forceinline__ void load(const double* x, int64_t /*ld*/, double (&v)[NC]) const {
         const double* row = x + (size_t)(live ? c : 0) * (size_t)ldr;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const int j0 = 4 * (lane + 64 * g);
+            const int j0 = 4 * (lane + L * g);
             if (FULL || j0 < d) {
                 const double4 q = *reinterpret_cast<const double4*>(row + j0);
                 v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
@@ -209,7 +232,7 @@ struct WaveChain {
         double* row = x + (size_t)c * (size_t)ldr;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const int j0 = 4 * (lane + 64 * g);
+            const int j0 = 4 * (lane + L * g);
             if (FULL || j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
                                                                                v[4 * g + 3]);
         }
@@ -229,7 +252,7 @@ struct WaveChain {
         double* row = base + ((size_t)kk * (size_t)s.C + (size_t)c) * (size_t)ldr;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const int j0 = 4 * (lane + 64 * g);
+            const int j0 = 4 * (lane + L * g);
             if (FULL || j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2],
                                                                                v[4 * g + 3]);
         }

@@ -16,7 +16,8 @@
  * Each function names the reference lines it follows.  Arithmetic order is the
  * build's specification: sums left to right over coordinates
  * (order 0, lane-per-chain kernels) or per-lane partials + xor butterfly over 64
- * lanes (order 1, wave-per-chain kernels).
+ * lanes (order 1, wave-per-chain kernels); order W > 1: a chain spread over W waves (lane l of 64 W owns
+ * 4 (l + 64 W k) + e), each wave's butterfly, then the W wave sums left to right (block-per-chain kernels).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -82,7 +83,8 @@ static const double ORC_TWOPI = 0x1.921fb54442d18p+2;
 
 /* ------------------------------------------------------------ reductions */
 /* order 1: lane l of a 64-lane wave owns coordinates 4*(l + 64k) + e, e = 0..3, k = 0,1,...;
-   each lane accumulates its coordinates in (k, e) order, then xor butterfly 32,16,...,1. */
+   each lane accumulates its coordinates in (k, e) order, then xor butterfly 32,16,...,1.
+   order W > 1: lane l of 64 W owns 4*(l + 64 W k) + e; butterfly per wave, wave sums left to right. */
 static double orc_butterfly(double p[64]) {
     for (int off = 32; off >= 1; off >>= 1) {
         double q[64];
@@ -109,14 +111,20 @@ static double orc_dot(const double* v, const orc_model* mdl, int order) {
         for (int j = 0; j < d; ++j) a = fma(v[j], v[j], a);
         return a;
     }
-    double p[64];
-    for (int l = 0; l < 64; ++l) {
-        double a = 0.0;
-        for (int j0 = 4 * l; j0 < d; j0 += 256)
-            for (int e = 0; e < 4 && j0 + e < d; ++e) a = fma(v[j0 + e], v[j0 + e], a);
-        p[l] = a;
+    const int W = order, L = 64 * order;          /* W waves per chain, lane l owns 4 (l + L k) + e */
+    double tot = 0.0;
+    for (int w = 0; w < W; ++w) {
+        double p[64];
+        for (int l = 0; l < 64; ++l) {
+            double a = 0.0;
+            for (int j0 = 4 * (64 * w + l); j0 < d; j0 += 4 * L)
+                for (int e = 0; e < 4 && j0 + e < d; ++e) a = fma(v[j0 + e], v[j0 + e], a);
+            p[l] = a;
+        }
+        const double sw = orc_butterfly(p);
+        tot = w == 0 ? sw : tot + sw;             /* waves left to right */
     }
-    return orc_butterfly(p);
+    return tot;
 }
 
 static double orc_sum(const double* t, const orc_model* mdl, int order) {
@@ -130,14 +138,20 @@ static double orc_sum(const double* t, const orc_model* mdl, int order) {
         for (int j = 0; j < d; ++j) a = a + t[j];
         return a;
     }
-    double p[64];
-    for (int l = 0; l < 64; ++l) {
-        double a = 0.0;
-        for (int j0 = 4 * l; j0 < d; j0 += 256)
-            for (int e = 0; e < 4 && j0 + e < d; ++e) a = a + t[j0 + e];
-        p[l] = a;
+    const int W = order, L = 64 * order;
+    double tot = 0.0;
+    for (int w = 0; w < W; ++w) {
+        double p[64];
+        for (int l = 0; l < 64; ++l) {
+            double a = 0.0;
+            for (int j0 = 4 * (64 * w + l); j0 < d; j0 += 4 * L)
+                for (int e = 0; e < 4 && j0 + e < d; ++e) a = a + t[j0 + e];
+            p[l] = a;
+        }
+        const double sw = orc_butterfly(p);
+        tot = w == 0 ? sw : tot + sw;
     }
-    return orc_butterfly(p);
+    return tot;
 }
 
 /* ------------------------------------------------------------ regression models (MFMA kernels) */

@@ -150,8 +150,31 @@ def assert_parity(chain, s_ref, g_ref, acc_ref, kind):
 
 
 def order_for(d):
-    """lane-per-chain kernels (d <= 32) sum left to right; wave-per-chain kernels per lane + butterfly."""
-    return 0 if d <= 32 else 1
+    """lane-per-chain kernels (d <= 32) sum left to right; wave-per-chain kernels (d <= 2048) per lane + butterfly;
+    block-per-chain kernels (d <= 8192: 4 waves, d <= 16384: 8 waves) per lane, per wave, then waves left to right."""
+    return 0 if d <= 32 else 1 if d <= 2048 else 4 if d <= 8192 else 8
+
+
+@pytest.mark.parametrize("sname", list(SAMPLERS))
+@pytest.mark.parametrize("mkind", ["iso", "normal"])
+@pytest.mark.parametrize("d", [2049, 5000, 8192, 8193, 16384])
+def test_block_per_chain_parity(gpu, sname, mkind, d):
+    """d > 2048 (the reference's model() takes any d, likmodel.jl:100-143): one chain per block of 4 (d <= 8192) or
+    8 (d <= 16384) waves, sums per lane, per wave, then over the waves -- bitwise against the oracle in that order,
+    every sampler, both separable model families, partial and full last blocks."""
+    m = _model(mkind, d)
+    C = 5
+    r = mc.SerialMC(steps=6, burnin=1, thinning=2)
+    t = (m * SAMPLERS[sname]() * r).batch(C, seed=2024 + d)
+    chain = mc.run(t)
+    assert t.step_kernel.startswith("bpc_")
+    oc = orc.OracleChains(m, SAMPLERS[sname](), nchains=C, seed=2024 + d, order=order_for(d))
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, sname)
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    lp, g = m.evalallg(chain.final_x)                       # model.eval at this d (bpc_eval)
+    lp_r, g_r = orc.eval_batch(m, chain.final_x, order=order_for(d))
+    assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
 
 
 @pytest.mark.parametrize("sname", list(SAMPLERS))
