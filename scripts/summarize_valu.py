@@ -10,7 +10,7 @@ pass and derives:
     the profiles SQ_BUSY_CU_CYCLES counts plain cycles summed over CUs (it equals CUs x the dispatch
     duration x the clock that GRBM_GUI_ACTIVE / duration gives), so the ratio needs no further factor.
     This is rocprof's VALUBusy with the dispatch's own busy cycles in place of GRBM_GUI_ACTIVE.
-  - the instruction mix per wave-step and the quad-cycles per VALU instruction.
+  - the instruction mix per 64 chain-steps (a lane-per-chain wave-step) and the quad-cycles per VALU instruction.
   - clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration.
 Writes profiles/<tag>.md and records the per-chain-step figures in profiles/valu.json for bench.py
 (keyed by kernel name: the per-chain-step VALU quad-cycles do not depend on the step count).
@@ -64,10 +64,10 @@ L = [f"# VALU roofline: {tag}", "", f"kernel: `{kname}`", f"workload: `{bl['conf
      f"timed dispatch: {dur * 1e3:.3f} ms; clock (GRBM_GUI_ACTIVE / 8 XCDs / duration) {clock:.2f} GHz; "
      f"CU busy {cu_cycles:.4g} cycles per CU ({cu_cycles / (dur * clock * 1e9):.3f} of the dispatch)", "",
      f"- **VALU busy = SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES = {busy:.3f}**",
-     f"- VALU instructions per wave-step: {entry['valu_insts_per_wave_step']:.1f}; "
+     f"- VALU instructions per 64 chain-steps (one wave-step of a lane-per-chain kernel): {entry['valu_insts_per_wave_step']:.1f}; "
      f"quad-cycles per VALU instruction: {entry['quadcycles_per_valu_inst']:.3f}; "
      f"dual-issue quad-cycles (SQ_ACTIVE_INST_VALU2) / SQ_ACTIVE_INST_VALU: {entry['dual_issue_frac']:.4f}", "",
-     "| counter | timed dispatch | per wave-step |", "|---|---|---|"]
+     "| counter | timed dispatch | per 64 chain-steps |", "|---|---|---|"]
 for c in sorted(v):
     L.append(f"| {c} | {v[c]:.6g} | {v[c] / waves / steps:.2f} |")
 open(os.path.join(root, "profiles", f"{tag}.md"), "w").write("\n".join(L) + "\n")
