@@ -431,11 +431,15 @@ def main():
         per_step, per_kept = hbm_bytes_per_unit(d, args.sampler)
         state_b = 2 * C * (8 * d + 8)                  # x [d][C] and lp [C], read and written
         fused = launches * state_b + C * nkept * (per_kept + 1 / 8)
+        if args.sampler == "ram":
+            # the jump factor S (d(d+1)/2 doubles per chain) does not fit on chip: read and written every step
+            fused += C * K * 8 * d * (d + 1)
         hbm_ach = fused / launches / avg_launch_s / 1e9
         survey = C * K * per_step + C * nkept * per_kept
         hbm = {"achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
                "algorithmic_bytes_per_launch": fused / launches, "traffic": traffic, "traffic_detail": tdet,
-               "note": "fused design: chain state in and out once per launch + kept samples/gradients + accept bits"}
+               "note": "fused design: chain state in and out once per launch + kept samples/gradients + accept bits"
+                       + (" + the RAM jump factor read and written every step" if args.sampler == "ram" else "")}
         survey_bytes = {"bytes_per_unit": {"chain_step": per_step, "kept_chain_step": per_kept},
                         "equivalent_GBps": survey / launches / avg_launch_s / 1e9,
                         "note": "SURVEY.md §8(d) bytes of an unfused step (state round trip every step); the "

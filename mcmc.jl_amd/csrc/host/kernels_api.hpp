@@ -57,6 +57,7 @@ int mcmc_glm_d_pad(int d);
 int mcmc_glm_steps_per_launch(int d, int64_t n, int sampler_kind);
 
 hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st);
+hipError_t mcmc_fill_f64_strided(double* p, int64_t nb, int64_t w, int64_t stride, double v, hipStream_t st);
 hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st);
 hipError_t mcmc_broadcast_cols(double* dst, int64_t ldd, const double* v, int d, int64_t C, hipStream_t st);
 hipError_t mcmc_broadcast_rows(double* dst, int64_t ldr, const double* v, int d, int64_t C, hipStream_t st);

@@ -572,13 +572,14 @@ static int init_state(mcmc_chains* c) {
         HIP_TRY(mcmc_fill_f64(c->st.t_h, c->C, 0.0, st));       // dualH = 0.
     }
     if (sa.kind == SK_RAM) {
-        // S = diag(model.scale .* sampler.scale) (RAM.jl:51,55) in half 0: packed rows, diagonal (r, r)
-        // at r(r+1)/2 + r; the padding block d..dpad-1 is the identity
+        // S = diag(model.scale .* sampler.scale) (RAM.jl:51,55) in half 0: packed rows in 64-chain tiles
+        // (ram.hpp), diagonal (r, r) at row r(r+1)/2 + r of every tile; the padding block d..dpad-1 is the identity
         const int64_t rl = c->st.ram_ld;
+        const int64_t tile = (int64_t)(ram_nrows(c->ram_dpad) + 1) * 64;
         HIP_TRY(hipMemsetAsync(c->st.ram_L, 0, 2 * (ram_nrows(c->ram_dpad) + 1) * (size_t)rl * 8, st));
         for (int r = 0; r < c->ram_dpad; ++r)
-            HIP_TRY(mcmc_fill_f64(c->st.ram_L + (size_t)(r * (r + 1) / 2 + r) * rl, rl,
-                                  r < d ? c->h_scale_eff[r] : 1.0, st));
+            HIP_TRY(mcmc_fill_f64_strided(c->st.ram_L + (size_t)(r * (r + 1) / 2 + r) * 64, rl / 64, 64, tile,
+                                          r < d ? c->h_scale_eff[r] : 1.0, st));
     }
     if (sa.tuner) {
         HIP_TRY(mcmc_fill_i32(c->st.t_acc, c->C, 0, st));
@@ -732,10 +733,14 @@ extern "C" int mcmc_chains_ram_factor(mcmc_chains* c, double* S) {
     if (int r = set_device(ctx)) return r;
     const size_t rows = ram_nrows(c->model->args.d);          // the leading rows of the padded packing
     const size_t rl = (size_t)c->st.ram_ld;
+    const size_t tile = (ram_nrows(c->ram_dpad) + 1) * 64;    // one 64-chain tile of a half (ram.hpp)
     const double* cur = c->st.ram_L + (size_t)(c->steps_done & 1) * (ram_nrows(c->ram_dpad) + 1) * rl;   // written last
-    HIP_TRY(hipMemcpy2DAsync(S, (size_t)c->C * 8, cur, rl * 8, (size_t)c->C * 8, rows,
-                             hipMemcpyDeviceToHost, ctx->stream));
+    const size_t ntiles = ((size_t)c->C + 63) / 64;
+    std::vector<double> h(ntiles * tile);
+    HIP_TRY(hipMemcpyAsync(h.data(), cur, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (size_t r = 0; r < rows; ++r)                          // [tile][row][64] -> [row][chain]
+        for (size_t ch = 0; ch < (size_t)c->C; ++ch) S[r * (size_t)c->C + ch] = h[(ch >> 6) * tile + r * 64 + (ch & 63)];
     return MCMC_OK;
 }
 

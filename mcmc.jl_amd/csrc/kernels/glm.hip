@@ -709,7 +709,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_rwm(GlmArgs a) {
 // full normal vector (every lane of the chain draws all DF/4 blocks), keeps it across the evaluation,
 // and after the accept updates its rows of every column k; the pivot u[k] comes from its owner by a
 // cross-lane read.  Rows r <= k of a column compute throw-away values whose stores go to the trash row
-// of the half (index ram_rows(DF)), so the loop carries no branches.
+// of the tile (index ram_rows(DF)), so the loop carries no branches.
 template <int NM, int NW>
 __global__ __launch_bounds__(glm_block<NW>()) void glm_ram(GlmArgs a) {
     static_assert(NW == 1, "RAM on regression targets is built for d <= 32");
@@ -722,8 +722,18 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_ram(GlmArgs a) {
     const Stream rs{s.key0, s.key1};
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
     f64x4 dummy[NM];
-    double* const Lc = a.st.ram_L + p.c;                        // own column (padding past the last chain)
+    // the wave's 16 chains lie in one 64-chain tile of the factor store (ram.hpp layout; padding chains past
+    // the last one), addressed through buffer resources: lane offset lo, own row r's base rowb[slot]
+    const uint32_t rtile = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * a.g.tpw + p.tile) >> 2));
+    double* const T0 = a.st.ram_L + (uint64_t)rtile * (uint64_t)ram_tile_doubles(DF);
     const uint64_t ld = (uint64_t)a.st.ram_ld;
+    const uint32_t lo = (uint32_t)(p.c & 63) * 8;
+    uint32_t rowb[NS];
+#pragma unroll
+    for (int slot = 0; slot < NS; ++slot) {
+        const int r = own_coord(p, slot);
+        rowb[slot] = lo + (uint32_t)(r * (r + 1) / 2) * 512;
+    }
     const int d = s.d;
     double lp = a.st.lp[p.live ? p.c : 0];
     for (int t = 0; t < s.nsteps; ++t) {
@@ -743,17 +753,15 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_ram(GlmArgs a) {
             }
             double x[NS];
             glm_load<NM>(a, p, a.st.x, x);
-            const uint64_t ldo = ram_opaque(ld);
-            const double* Ls = ram_half<DF>(Lc, i - 1, ldo);
+            const ram_rsrc_t Rs = ram_tile_rsrc<DF>(ram_half<DF>(T0, i - 1, ld));
 #pragma unroll
             for (int slot = 0; slot < NS; ++slot) {
                 // own row r: the fma chain over c <= r, then exact no-ops fma(0, z, acc)
                 const int r = own_coord(p, slot);
-                const double* Lr = Ls + (uint64_t)(r * (r + 1) / 2) * ldo;
                 double acc = 0.0;
 #pragma unroll
                 for (int c = 0; c < DF; ++c) {
-                    const double v = Lr[(uint64_t)c * ldo];
+                    const double v = ram_tload(Rs, rowb[slot], c);            // row r(r+1)/2 + c (in the tile)
                     acc = __builtin_fma(c <= r ? v : 0.0, z[c], acc);
                 }
                 u[slot] = acc;
@@ -781,33 +789,30 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_ram(GlmArgs a) {
         const double sb = __builtin_sqrt(__builtin_fabs(beta));
 #pragma unroll
         for (int slot = 0; slot < NS; ++slot) u[slot] = sb * u[slot];
-        const uint64_t ldu = ram_opaque(ld);
-        const double* Ls = ram_half<DF>(Lc, i - 1, ldu);
-        double* Ld = ram_half<DF>(Lc, i, ldu);
-        const uint64_t trash = (uint64_t)ram_rows(DF) * ldu;
+        const ram_rsrc_t Rs = ram_tile_rsrc<DF>(ram_half<DF>(T0, i - 1, ld));
+        const ram_rsrc_t Rd = ram_tile_rsrc<DF>(ram_half<DF>(T0, i, ld));
 #pragma unroll
         for (int k = 0; k < DF; ++k) {
             const int kslot = 4 * (k >> 4) + (k & 3);                           // owner: q = (k & 15) >> 2
             const double xk = __shfl(u[kslot], p.cl + 16 * ((k & 15) >> 2), 64);
-            const uint64_t okk = (uint64_t)(k * (k + 1) / 2 + k) * ldu;
-            const double lkk = Ls[okk];
+            const double lkk = ram_tload(Rs, lo, k * (k + 1) / 2 + k);
             const double t2 = xk * xk;
             const double l2 = lkk * lkk;
             const double r = __builtin_sqrt(up ? l2 + t2 : l2 - t2);
             const double cc = r / lkk;
             const double sn = xk / lkk;
+            const double sns = up ? sn : -sn;                                   // as ram.hpp ram_update
             const double ic = 1.0 / cc;
-            Ld[okk] = r;
+            ram_tstore(Rd, lo, k * (k + 1) / 2 + k, r);
 #pragma unroll
             for (int slot = 0; slot < NS; ++slot) {
                 const int q = own_coord(p, slot);
                 if (16 * (slot >> 2) + 12 + (slot & 3) <= k) continue;          // no row of this slot is below k
                 const bool below = q > k;
-                const uint64_t oq = (uint64_t)(q * (q + 1) / 2 + k) * ldu;     // in bounds for q <= k too
-                const double l0 = Ls[oq];
-                const double su = sn * u[slot];
-                const double l = (up ? l0 + su : l0 - su) * ic;
-                Ld[below ? oq : trash] = l;
+                const double l0 = ram_tload(Rs, rowb[slot], k);                // in bounds for q <= k too
+                const double l = (l0 + sns * u[slot]) * ic;
+                // rows q <= k store to the tile's trash row (index ram_rows(DF))
+                ram_tstore(Rd, below ? rowb[slot] : lo + (uint32_t)(ram_rows(DF) - k) * 512, k, l);
                 const double un = cc * u[slot] - sn * l;
                 u[slot] = below ? un : u[slot];
             }

@@ -9,6 +9,11 @@ __global__ void k_fill_f64(double* p, int64_t n, double v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
 }
+// p[b * stride + e] = v, e < w, b < nb
+__global__ void k_fill_f64_strided(double* p, int64_t nb, int64_t w, int64_t stride, double v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb * w) p[(i / w) * stride + i % w] = v;
+}
 __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -117,6 +122,11 @@ static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / 
 hipError_t mcmc_fill_f64(double* p, int64_t n, double v, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     mcmc::k_fill_f64<<<nblk(n, 256), 256, 0, st>>>(p, n, v);
+    return hipGetLastError();
+}
+hipError_t mcmc_fill_f64_strided(double* p, int64_t nb, int64_t w, int64_t stride, double v, hipStream_t st) {
+    if (nb <= 0 || w <= 0) return hipSuccess;
+    mcmc::k_fill_f64_strided<<<nblk(nb * w, 256), 256, 0, st>>>(p, nb, w, stride, v);
     return hipGetLastError();
 }
 hipError_t mcmc_fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t st) {

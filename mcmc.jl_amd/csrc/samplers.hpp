@@ -704,22 +704,27 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
     double x[NC];
     p.load(a.st.x, s.ld, x);
     double lp = p.load_scalar(a.st.lp);
-    const uint32_t col = (uint32_t)p.c;                        // own column (padding past the last chain)
+    // the wave's 64-chain tile of each half of the factor store (ram.hpp), as buffer resources
     const uint64_t ld = (uint64_t)a.st.ram_ld;
+    const uint32_t tile = (uint32_t)blockIdx.x * (kBlock / 64) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double* const T0 = a.st.ram_L + (uint64_t)tile * (uint64_t)ram_tile_doubles(NC);
+    const uint32_t vo = (threadIdx.x & 63) * 8;
+    // rvec = randn(d) of step i and its S * rvec: the launch's first step forms them here, every later one
+    // inside the previous step's factor update (ram_update<NEXT = true>), so a step reads the factor once
+    double u[NC], nz = 0.0;
+    if (s.nsteps > 0) {
+        const int64_t i = s.step_begin;
+        double z[NC];
+        gen_normals(p, rs, chain, (uint32_t)i, z);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (!p.valid(k)) z[k] = 0.0;                                    // padding: identity block
+            nz = __builtin_fma(z[k], z[k], nz);                             // dot(rvec, rvec)
+        }
+        ram_matvec<NC>(ram_tile_rsrc<NC>(ram_half<NC>(T0, i - 1, ld)), vo, z, u);
+    }
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
-        const uint64_t ldo = ram_opaque(ld);
-        double u[NC], nz = 0.0;
-        {
-            double z[NC];
-            gen_normals(p, rs, chain, (uint32_t)i, z);                          // rvec = randn(d)
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                if (!p.valid(k)) z[k] = 0.0;                                    // padding: identity block
-                nz = __builtin_fma(z[k], z[k], nz);                             // dot(rvec, rvec)
-            }
-            ram_matvec<NC>(ram_half<NC>(a.st.ram_L, i - 1, ldo), col, ldo, z, u);   // S * rvec
-        }
         double lpp;
         {
             double xp[NC];
@@ -741,9 +746,27 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
             p.store_kept(s, kk, x, s.samples);
             p.store_bit(s, kk, acc);
         }
-        const uint64_t ldu = ram_opaque(ld);       // fresh: no offset products live across the evaluation
-        ram_update<NC>(ram_half<NC>(a.st.ram_L, i - 1, ldu), ram_half<NC>(a.st.ram_L, i, ldu), col, ldu,
-                       ram_alpha(i, s.d, ratio, sa.rate), nz, u);
+        const double alpha = ram_alpha(i, s.d, ratio, sa.rate);
+        const ram_rsrc_t Ss = ram_tile_rsrc<NC>(ram_half<NC>(T0, i - 1, ld));
+        const ram_rsrc_t Sd = ram_tile_rsrc<NC>(ram_half<NC>(T0, i, ld));
+        double un[NC], nzn = 0.0;
+        auto zblock = [&](int b, double (&z4)[4]) {                           // step i + 1's rvec, block b
+            const u32x4 w = rs.block(chain, (uint32_t)(i + 1), p.block(b), TAG_NORMAL);
+            normals4(w, z4[0], z4[1], z4[2], z4[3], p.tab, p.sct);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!p.valid(4 * b + e)) z4[e] = 0.0;
+                nzn = __builtin_fma(z4[e], z4[e], nzn);
+            }
+        };
+        if (t + 1 < s.nsteps) {
+            ram_update<NC, true>(Ss, Sd, vo, alpha, nz, u, zblock, un);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) u[k] = un[k];
+            nz = nzn;
+        } else {
+            ram_update<NC, false>(Ss, Sd, vo, alpha, nz, u, zblock, un);
+        }
     }
     p.store(a.st.x, s.ld, x);
     p.store_t(a.st.lp, lp);

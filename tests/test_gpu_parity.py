@@ -482,7 +482,7 @@ def _assert_ram_factor(task, oc, d):
 
 
 @pytest.mark.parametrize("mkind", ["iso", "normal", "abs", "dist"])
-@pytest.mark.parametrize("d", [1, 3, 7, 16, 17, 32])
+@pytest.mark.parametrize("d", [1, 3, 7, 16, 17, 28, 30, 32])
 def test_ram_parity(gpu, mkind, d):
     """lane-per-chain RAM: samples, accept bits, final state and every chain's jump factor S bit-identical
     to the oracle (proposals out of the Gamma support -> -Inf -> downdates of S)."""
