@@ -56,6 +56,9 @@ CONFIGS = {
     # the adaptive RAM sampler (not a BASELINE config)
     "ram32": dict(model="iso", d=32, chains=1 << 18, sampler="ram", steps=200, warmup=20, thinning=10,
                   desc="RAM(1., 0.234) on d=32 iso-Normal, 262,144 chains (a 32x32 jump factor per chain)"),
+    "ram256": dict(model="iso", d=256, chains=1 << 16, sampler="ram", steps=100, warmup=10, thinning=10,
+                   desc="RAM(1., 0.234) on d=256 iso-Normal, 65,536 chains (wave per chain, a 256x256 jump factor "
+                        "per chain)"),
     "ramlinear": dict(model="linear", d=10, n=1000, chains=1 << 16, sampler="ram", steps=200, warmup=20,
                       thinning=10, desc="examples/linear_regression.jl:28: RAM(1., 0.3), n=1000 d=10, "
                                         "65,536 chains"),

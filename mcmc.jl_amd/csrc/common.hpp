@@ -55,7 +55,9 @@ struct ChainState {
     int32_t* t_acc;             // tuner accepted counter
     int32_t* t_prop;            // tuner proposed counter
     double* ram_L;              // RAM: jump factor S, two halves of packed padded rows [dpad(dpad+1)/2][ram_ld]
-    int64_t ram_ld;             // RAM: chain stride of ram_L (a multiple of 256)
+    int64_t ram_ld;             // RAM: lane-per-chain: chain stride of ram_L (a multiple of 256); wave-per-chain:
+                                //      doubles per chain (ram.hpp wave layout)
+    int64_t ram_hs;             // RAM: doubles from the first half of ram_L to the second
 };
 
 // One launch of the fused step kernel.

@@ -30,6 +30,7 @@ hipError_t mcmc_launch_wpc_step(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_launch_wpc_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_wpc_max_d();
+int mcmc_wpc_ram_max_d();
 // regression models on fp64 MFMA, state [d][ld] (+ gradient [d][ld])
 hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& a, hipStream_t st);
 // storeLeaps: record the trajectory of the next step (HMC / HMCDA) without moving the chains

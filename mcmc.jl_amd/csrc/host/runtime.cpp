@@ -447,6 +447,8 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // RAM jump factor (ram.hpp): packed lower-triangular rows padded to the kernel's width + a trash row,
 // two halves
 static size_t ram_nrows(int d) { return (size_t)d * (size_t)(d + 1) / 2; }
+// first element of column k in the wave layout's column-major packing (ram.hpp ram_wave_colstart)
+static int64_t wave_colstart(int64_t k, int64_t d) { return k * d - k * (k - 1) / 2; }
 
 // State layout of a chain batch: lane-per-chain [d][ld] for d <= 32, wave-per-chain [C][ld] above.
 static Layout layout_for(const mcmc_model* m) {
@@ -575,11 +577,17 @@ static int init_state(mcmc_chains* c) {
         // S = diag(model.scale .* sampler.scale) (RAM.jl:51,55) in half 0: packed rows in 64-chain tiles
         // (ram.hpp), diagonal (r, r) at row r(r+1)/2 + r of every tile; the padding block d..dpad-1 is the identity
         const int64_t rl = c->st.ram_ld;
-        const int64_t tile = (int64_t)(ram_nrows(c->ram_dpad) + 1) * 64;
-        HIP_TRY(hipMemsetAsync(c->st.ram_L, 0, 2 * (ram_nrows(c->ram_dpad) + 1) * (size_t)rl * 8, st));
-        for (int r = 0; r < c->ram_dpad; ++r)
-            HIP_TRY(mcmc_fill_f64_strided(c->st.ram_L + (size_t)(r * (r + 1) / 2 + r) * 64, rl / 64, 64, tile,
-                                          r < d ? c->h_scale_eff[r] : 1.0, st));
+        HIP_TRY(hipMemsetAsync(c->st.ram_L, 0, 2 * (size_t)c->st.ram_hs * 8, st));
+        if (c->layout == LAYOUT_WPC) {                     // diagonal (k, k) at colstart(k) of every chain block
+            for (int k = 0; k < d; ++k)
+                HIP_TRY(mcmc_fill_f64_strided(c->st.ram_L + wave_colstart(k, d), c->st.ram_hs / rl, 1, rl,
+                                              c->h_scale_eff[k], st));
+        } else {
+            const int64_t tile = (int64_t)(ram_nrows(c->ram_dpad) + 1) * 64;
+            for (int r = 0; r < c->ram_dpad; ++r)
+                HIP_TRY(mcmc_fill_f64_strided(c->st.ram_L + (size_t)(r * (r + 1) / 2 + r) * 64, rl / 64, 64, tile,
+                                              r < d ? c->h_scale_eff[r] : 1.0, st));
+        }
     }
     if (sa.tuner) {
         HIP_TRY(mcmc_fill_i32(c->st.t_acc, c->C, 0, st));
@@ -601,8 +609,12 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (nchains <= 0) return fail(MCMC_E_INVALID_ARG, "nchains should be > 0");
     if (chain_offset < 0 || chain_offset + nchains > (int64_t)0x100000000LL)
         return fail(MCMC_E_INVALID_ARG, "global chain ids must fit in 32 bits");
-    if (s->kind == MCMC_RAM && m->args.d > 32)
-        return fail(MCMC_E_UNSUPPORTED, "RAM is built for d <= 32 (the d x d jump factor of every chain is kept in HBM)");
+    if (s->kind == MCMC_RAM && !model_is_separable(m) && m->args.d > 32)
+        return fail(MCMC_E_UNSUPPORTED, "RAM on regression targets is built for d <= 32 (the d x d jump factor of every "
+                                        "chain is kept in HBM)");
+    if (s->kind == MCMC_RAM && m->args.d > mcmc_wpc_ram_max_d())
+        return fail(MCMC_E_UNSUPPORTED, "RAM is built for d <= " + std::to_string(mcmc_wpc_ram_max_d()) +
+                                        " (the d x d jump factor of every chain is kept in HBM)");
     if (s->kind != MCMC_RWM && s->kind != MCMC_RAM && !m->has_gradient) {
         const char* nm = s->kind == MCMC_MALA ? "MALA" : s->kind == MCMC_HMC ? "HMC" : "HMCDA";
         return fail(MCMC_E_NEEDS_GRADIENT, std::string(nm) + " sampler requires model with gradient function");
@@ -667,9 +679,17 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     c->h_scale_eff = se;
     if (sa.kind == SK_RAM) {
         // padded width: the lane-per-chain kernel's NC = 4 ceil(d/4), the regression kernel's DF = d_pad
-        c->ram_dpad = c->layout == LAYOUT_GLM ? mcmc_glm_d_pad(d) : (int)round_up(d, 4);
-        c->st.ram_ld = round_up(nchains, 256);
-        if (int r = dmalloc(&c->st.ram_L, 2 * (ram_nrows(c->ram_dpad) + 1) * (size_t)c->st.ram_ld)) return bail(r);
+        if (c->layout == LAYOUT_WPC) {
+            // wave-per-chain: [half][chain][column-major packed factor] (ram.hpp wave layout), 4-chain blocks
+            c->ram_dpad = d;
+            c->st.ram_ld = round_up((int64_t)ram_nrows(d), 8);
+            c->st.ram_hs = round_up(nchains, 4) * c->st.ram_ld;
+        } else {
+            c->ram_dpad = c->layout == LAYOUT_GLM ? mcmc_glm_d_pad(d) : (int)round_up(d, 4);
+            c->st.ram_ld = round_up(nchains, 256);
+            c->st.ram_hs = (int64_t)(ram_nrows(c->ram_dpad) + 1) * c->st.ram_ld;
+        }
+        if (int r = dmalloc(&c->st.ram_L, 2 * (size_t)c->st.ram_hs)) return bail(r);
     }
     c->scale1 = se.empty() ? 0.0 : se[0];
     c->scale_uniform = 1;
@@ -733,8 +753,19 @@ extern "C" int mcmc_chains_ram_factor(mcmc_chains* c, double* S) {
     if (int r = set_device(ctx)) return r;
     const size_t rows = ram_nrows(c->model->args.d);          // the leading rows of the padded packing
     const size_t rl = (size_t)c->st.ram_ld;
+    const double* cur = c->st.ram_L + (size_t)(c->steps_done & 1) * (size_t)c->st.ram_hs;   // written last
+    if (c->layout == LAYOUT_WPC) {                             // [chain][column-major packed] -> [row][chain]
+        const int64_t d = c->model->args.d;
+        std::vector<double> h((size_t)c->C * rl);
+        HIP_TRY(hipMemcpyAsync(h.data(), cur, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (int64_t r = 0; r < d; ++r)
+            for (int64_t q = 0; q <= r; ++q)
+                for (size_t ch = 0; ch < (size_t)c->C; ++ch)
+                    S[(size_t)(r * (r + 1) / 2 + q) * (size_t)c->C + ch] = h[ch * rl + (size_t)(wave_colstart(q, d) + r - q)];
+        return MCMC_OK;
+    }
     const size_t tile = (ram_nrows(c->ram_dpad) + 1) * 64;    // one 64-chain tile of a half (ram.hpp)
-    const double* cur = c->st.ram_L + (size_t)(c->steps_done & 1) * (ram_nrows(c->ram_dpad) + 1) * rl;   // written last
     const size_t ntiles = ((size_t)c->C + 63) / 64;
     std::vector<double> h(ntiles * tile);
     HIP_TRY(hipMemcpyAsync(h.data(), cur, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -21,3 +21,8 @@ hipError_t mcmc_lpc_ram_iso(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_lpc_ram_normal(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_lpc_ram_absnormal(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_lpc_ram_dist(const mcmc::KernelArgs& a, hipStream_t st);
+// wave-per-chain RAM kernels, 32 < d <= 1024 (wpc_ram.hip)
+hipError_t mcmc_wpc_ram_iso(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_wpc_ram_normal(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_wpc_ram_absnormal(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_wpc_ram_dist(const mcmc::KernelArgs& a, hipStream_t st);

@@ -5,6 +5,16 @@
 hipError_t mcmc_launch_wpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
     using namespace mcmc;
     if (a.s.d < 1 || a.s.d > 16384) return hipErrorInvalidValue;
+    if (a.sa.kind == SK_RAM) {
+        if (a.s.d > mcmc_wpc_ram_max_d()) return hipErrorInvalidValue;
+        switch (a.m.kind) {
+            case MK_ISO: return mcmc_wpc_ram_iso(a, st);
+            case MK_NORMAL: return mcmc_wpc_ram_normal(a, st);
+            case MK_ABS_NORMAL: return mcmc_wpc_ram_absnormal(a, st);
+            case MK_DIST: return mcmc_wpc_ram_dist(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (a.m.kind) {
         case MK_ISO: return mcmc_wpc_step_iso(a, st);
         case MK_NORMAL: return mcmc_wpc_step_normal(a, st);
@@ -40,3 +50,4 @@ hipError_t mcmc_launch_wpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec
 }
 
 int mcmc_wpc_max_d() { return 16384; }
+int mcmc_wpc_ram_max_d() { return 1024; }

@@ -1,0 +1,33 @@
+// wpc_ram.hip -- wave-per-chain RAM kernels (src/samplers/RAM.jl:41-79) for 32 < d <= 1024, every separable
+// model kind: samplers.hpp ram_wave_body over the ram.hpp wave layout of the jump factor.
+#include "wpc_impl.hpp"
+
+namespace mcmc {
+
+template <int G, class M>
+__global__ __launch_bounds__(kBlock) void wpc_ram(KernelArgs a) { ram_wave_body<WaveChain<G, false>, M>(a); }
+
+template <class M>
+static hipError_t wpc_ram_step(const KernelArgs& a, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    const int g = wpc_nb_for(a.s.d);
+    mcmc_note_step_kernel("wpc_ram<%d, %s>", g, M::kName);
+    switch (g) {
+        case 1: wpc_ram<1, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 2: wpc_ram<2, M><<<grid, kBlock, 0, st>>>(a); break;
+        case 4: wpc_ram<4, M><<<grid, kBlock, 0, st>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mcmc
+
+hipError_t mcmc_wpc_ram_iso(const mcmc::KernelArgs& a, hipStream_t st) { return mcmc::wpc_ram_step<mcmc::IsoDot>(a, st); }
+hipError_t mcmc_wpc_ram_normal(const mcmc::KernelArgs& a, hipStream_t st) {
+    return mcmc::wpc_ram_step<mcmc::NormalDSL>(a, st);
+}
+hipError_t mcmc_wpc_ram_absnormal(const mcmc::KernelArgs& a, hipStream_t st) {
+    return mcmc::wpc_ram_step<mcmc::AbsNormalDSL>(a, st);
+}
+hipError_t mcmc_wpc_ram_dist(const mcmc::KernelArgs& a, hipStream_t st) { return mcmc::wpc_ram_step<mcmc::DistDSL>(a, st); }

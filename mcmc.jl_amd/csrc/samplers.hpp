@@ -773,6 +773,91 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
     p.count_evals(s, s.nsteps);
 }
 
+// Robust adaptive Metropolis for 32 < d <= 1024, wave per chain (ram.hpp wave layout): the lane-per-chain
+// body's steps with the factor's rows spread over the wave's lanes.
+template <class P, class M>
+__device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const P p(s);
+    const M model(a.m);
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    constexpr int NC = P::NC;
+    constexpr int G = P::NB;
+    const int d = s.d;
+    double x[NC];
+    p.load(a.st.x, s.ld, x);
+    double lp = p.load_scalar(a.st.lp);
+    // the chain's factor block in each half (the chain index is wave-uniform)
+    const int64_t cu = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    double* const B0 = a.st.ram_L + (uint64_t)cu * (uint64_t)a.st.ram_ld;
+    const uint64_t hs = (uint64_t)a.st.ram_hs;
+    const int64_t ld = a.st.ram_ld;
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t vo = (uint32_t)lane * 32;
+    double u[NC], nz;
+    if (s.nsteps > 0) {
+        const int64_t i = s.step_begin;
+        double z[NC];
+        gen_normals(p, rs, chain, (uint32_t)i, z);
+        double a2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (!p.valid(k)) z[k] = 0.0;
+            a2 = __builtin_fma(z[k], z[k], a2);                               // dot(rvec, rvec)
+        }
+        nz = p.reduce(a2);
+        ram_wave_matvec<G>(ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld), vo, lane, d, z, u);
+    }
+    for (int t = 0; t < s.nsteps; ++t) {
+        const int64_t i = s.step_begin + t;
+        double lpp;
+        {
+            double xp[NC];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) xp[k] = x[k] + u[k];                 // RAM.jl:60
+            bool oos;
+            lpp = eval_lp(p, model, xp, oos);
+        }
+        const double ratio = lpp - lp;
+        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        if (acc) {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) x[k] = x[k] + u[k];
+            lp = lpp;
+        }
+        int64_t kk;
+        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+            p.store_kept(s, kk, x, s.samples);
+            p.store_bit(s, kk, acc);
+        }
+        const double alpha = ram_alpha(i, d, ratio, sa.rate);
+        const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld);
+        const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, ld);
+        if (t + 1 < s.nsteps) {
+            double zn[NC], un[NC];
+            gen_normals(p, rs, chain, (uint32_t)(i + 1), zn);                  // step i + 1's rvec
+            double a2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                if (!p.valid(k)) zn[k] = 0.0;
+                a2 = __builtin_fma(zn[k], zn[k], a2);
+            }
+            ram_wave_update<G, true>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) u[k] = un[k];
+            nz = p.reduce(a2);
+        } else {
+            double zn[NC], un[NC];
+            ram_wave_update<G, false>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
+        }
+    }
+    p.store(a.st.x, s.ld, x);
+    p.store_t(a.st.lp, lp);
+    p.count_evals(s, s.nsteps);
+}
+
 // ------------------------------------------------------------------ eval
 // lp (and gradient) of x; flags out-of-support starts (RWM.jl:54-55).
 template <class P, class M>

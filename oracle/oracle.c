@@ -548,8 +548,11 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
             /* RAM.jl:58-78 */
             double* Lc = st->ram_L + c;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* rvec = randn(d) */
-            double nz = 0.0;
-            for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);         /* dot(rvec, rvec) */
+            double nz = 0.0;                                                  /* dot(rvec, rvec): in order, */
+            if (order == 0 || orc_is_glm(m))                                  /* or in the wave order of the */
+                for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);     /* wave-per-chain kernel (d > 32) */
+            else
+                nz = orc_dot(mom, m, order);
             for (int r = 0; r < d; ++r) {                                     /* S * rvec */
                 double a = 0.0;
                 for (int q = 0; q <= r; ++q) a = fma(Lc[(size_t)(r * (r + 1) / 2 + q) * C], mom[q], a);

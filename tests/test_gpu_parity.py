@@ -540,12 +540,32 @@ def test_ram_continue_spl_and_shards(gpu):
     assert np.array_equal(np.concatenate([lo._samples, hi._samples], axis=2), s)
 
 
+@pytest.mark.parametrize("mkind", ["iso", "normal", "abs", "dist"])
+@pytest.mark.parametrize("d", [33, 64, 100, 256, 257, 513, 1024])
+def test_ram_wave_parity(gpu, mkind, d):
+    """32 < d <= 1024 (RAM.jl:41-80 has no d cap): wave-per-chain RAM, the factor column-major per chain and its
+    rows spread over the lanes; samples, accept bits, final state and every factor bit-identical to the oracle in
+    the wave order (d <= 256: one slot group per lane, 257..512: two, 513..1024: four; tail wave and tail block)."""
+    m = _ram_model(mkind, d)
+    C = 7
+    r = mc.SerialMC(steps=14 if d <= 256 else 8, burnin=2, thinning=2)
+    task = (m * mc.RAM(0.7, 0.3) * r).batch(C, seed=777 + d, steps_per_launch=5)
+    chain = mc.run(task)
+    assert task.step_kernel.startswith("wpc_ram<")
+    oc = orc.OracleChains(m, mc.RAM(0.7, 0.3), nchains=C, seed=777 + d, order=order_for(d))
+    s_ref, _, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, None, acc_ref, "ram")
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert task.evals == int(oc.n_evals.sum())
+    _assert_ram_factor(task, oc, d)
+
+
 def test_ram_limits(gpu):
-    m = _model("iso", 33)
-    with pytest.raises(mc.MCMCError, match="RAM is built for d <= 32"):
+    m = _model("iso", 1025)
+    with pytest.raises(mc.MCMCError, match="RAM is built for d <= 1024"):
         mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
     m = _glm_model("linear", 40)
-    with pytest.raises(mc.MCMCError, match="RAM is built for d <= 32"):
+    with pytest.raises(mc.MCMCError, match="RAM on regression targets is built for d <= 32"):
         mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
 
 
