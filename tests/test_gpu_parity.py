@@ -560,6 +560,25 @@ def test_ram_wave_parity(gpu, mkind, d):
     _assert_ram_factor(task, oc, d)
 
 
+def test_ram_wave_continue_and_shards(gpu):
+    """wave-per-chain RAM: the factor lives on the device between runs, and chain offsets are invisible"""
+    d = 70
+    m = _model("normal", d)
+    r = mc.SerialMC(steps=12, burnin=2, thinning=3)
+    task = (m * mc.RAM() * r).batch(9, seed=21)
+    c1 = mc.run(task)
+    c2 = mc.run(c1)
+    oc = orc.OracleChains(m, mc.RAM(), nchains=9, seed=21, order=order_for(d))
+    s1, _, a1 = oc.run(r)
+    s2, _, a2 = oc.run(r)
+    assert_parity(c1, s1, None, a1, "ram")
+    assert_parity(c2, s2, None, a2, "ram")
+    _assert_ram_factor(task, oc, d)
+    lo = mc.run((m * mc.RAM() * r).batch(5, seed=21))
+    hi = mc.run((m * mc.RAM() * r).batch(4, seed=21, chain_offset=5))
+    assert np.array_equal(np.concatenate([lo._samples, hi._samples], axis=2), s1)
+
+
 def test_ram_limits(gpu):
     m = _model("iso", 1025)
     with pytest.raises(mc.MCMCError, match="RAM is built for d <= 1024"):
