@@ -11,7 +11,9 @@ HBM before the clock starts.
 
 Other BASELINE.json configs (--config): readme (config 1), d3 (config 2),
 logistic128 (config 3), hmc1024 (config 4, per-GPU shard), linear512
-(config 5, per-GPU shard).
+(config 5, per-GPU shard); binomial is the reference's own published benchmark
+unit (benchmarks/benchunits/binomial.jl: logistic n=1000, d=10, RWM(0.1), 100
+steps), printed beside its benchlog.csv numbers.
 
   python bench.py [--config metric] [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU; weak scaling:
@@ -50,9 +52,16 @@ CONFIGS = {
     "hmc1024": dict(model="iso", d=1024, chains=524288 // 8, sampler="hmc", steps=1000, warmup=100,
                     thinning=20, desc="config 4: d=1024 iso-Normal, HMC(10, 0.1), 524,288 chains over 8 GPUs "
                                        "(65,536/GPU)"),
-    "linear512": dict(model="linear", d=512, n=4096, chains=65536 // 8, sampler="hmcda", steps=20, warmup=2,
-                      thinning=1, desc="config 5: linear regression n=4096 d=512, HMCDA(), 65,536 chains over 8 "
-                                       "GPUs (8,192/GPU); 20 steps: each step is ~len/eps leapfrogs"),
+    "linear512": dict(model="linear", d=512, n=4096, chains=65536 // 8, sampler="hmcda", steps=20, warmup=100,
+                      thinning=1, adapt=True,
+                      desc="config 5: linear regression n=4096 d=512, HMCDA(), 65,536 chains over 8 GPUs (8,192/GPU); "
+                           "the configured burnin (100 steps of dual averaging, HMCDA.jl:133-138) runs untimed as the "
+                           "warmup, then the timed steps run at each chain's adapted dualLeapStep: a step is "
+                           "round(len/eps) leapfrogs of that chain (HMCDA.jl:104)"),
+    # the reference's own published benchmark unit (benchmarks/benchunits/binomial.jl:1-25, benchlog.csv:350-352)
+    "binomial": dict(model="logistic", d=10, n=1000, chains=1 << 18, sampler="rwm", steps=100, warmup=10,
+                     thinning=1, desc="benchmarks/benchunits/binomial.jl: logistic regression n=1000 d=10, "
+                                      "RWM(0.1), 100 steps (the reference's published unit, run batched)"),
     # the adaptive RAM sampler (not a BASELINE config)
     "ram32": dict(model="iso", d=32, chains=1 << 18, sampler="ram", steps=200, warmup=20, thinning=10,
                   desc="RAM(1., 0.234) on d=32 iso-Normal, 262,144 chains (a 32x32 jump factor per chain)"),
@@ -165,16 +174,19 @@ def step_kernel_src_hash():
     return h.hexdigest()[:16]
 
 
-def measured_valu(kname):
+def measured_valu(kname, wkey):
     """VALU issue cost of the step kernel per chain-step (SQ_ACTIVE_INST_VALU quad-cycles / chain-steps of the
     timed dispatch) and its measured VALU-busy fraction, from a committed rocprofv3 PMC run of this kernel
-    instance built from these sources (profiles/valu.json, written by scripts/summarize_valu.py), or None."""
+    instance, built from these sources, on this same workload (profiles/valu.json, written by
+    scripts/summarize_valu.py), or None.  The workload must match: per-launch work (table staging, state load
+    and store) is spread over the launch's steps, so a 20-step profile does not price a 1000-step run."""
     p = os.path.join(ROOT, "profiles", "valu.json")
     if not os.path.exists(p):
         return None
     h = step_kernel_src_hash()
     for k, e in json.load(open(p)).items():
-        if _norm_kernel(k) == _norm_kernel(kname) and e.get("src_hash") == h:
+        if (_norm_kernel(e.get("kernel", k)) == _norm_kernel(kname) and e.get("src_hash") == h
+                and e.get("workload_key") == wkey):
             return e
     return None
 
@@ -233,6 +245,50 @@ def cpu_baseline(model, sampler, seconds, C=4096):
                       f"so the rate is per chain-step)"}
 
 
+def binomial_units(mc, model, C, local):
+    """The reference's benchmark unit benchmarks/benchunits/binomial.jl:21-27 on this build, for context beside
+    benchlog.csv:350-352 (0.258 ms loglik eval, 0.748 ms loglik + gradient, 25.69 ms per 100 RWM steps of one
+    chain; 2-core Windows CPU, 2013): the host API's batched model.eval / model.evalallg (mcmc_model_eval: host
+    arrays in and out, PCIe included) over C parameter vectors and over one, and `run(m * RWM(0.1), steps=100)`
+    of one chain (SerialMC(steps=100), every sample kept, returned to the host)."""
+    import ctypes as ct
+    from mcmchip import _lib
+    lib = _lib.load()
+    d = model.size
+    mh = model._handle(local)
+    out = {}
+    for n in (1, C):
+        x = np.ascontiguousarray(np.repeat(model.init[:, None], n, axis=1))
+        lp = np.empty(n)
+        g = np.empty((d, n))
+        for name, gp in (("eval", None), ("evalallg", g)):
+            gptr = gp.ctypes.data_as(ct.POINTER(ct.c_double)) if gp is not None else None
+            args = (mh, n, x.ctypes.data_as(ct.POINTER(ct.c_double)), lp.ctypes.data_as(ct.POINTER(ct.c_double)), gptr)
+            _lib.check(lib.mcmc_model_eval(*args))
+            reps = 20 if n == 1 else 5
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                _lib.check(lib.mcmc_model_eval(*args))
+            dt = (time.perf_counter() - t0) / reps
+            out[f"{name}_{'1' if n == 1 else 'batch'}"] = {"points": n, "call_ms": dt * 1e3,
+                                                            "us_per_point": dt * 1e6 / n}
+    r = mc.SerialMC(steps=100)
+    t1 = mc.MCMCTask(model, mc.RWM(0.1), r, nchains=1, seed=1, device=local)
+    mc.run(t1)
+    times = []
+    for _ in range(10):                                   # benchmark(f3, "100 RWM steps", name, 10)
+        t1.reset()
+        t0 = time.perf_counter()
+        mc.run(t1)
+        times.append(time.perf_counter() - t0)
+    out["rwm100_1chain_ms"] = {"avg": 1e3 * sum(times) / len(times), "min": 1e3 * min(times)}
+    out["reference"] = {"source": "benchmarks/benchlog.csv:350-352 (binomial 10x1000, CodeHash 276db306bb, "
+                                  "Windows, 2 CPU cores, 2013-08-29)",
+                        "eval_ms": 0.25765, "evalallg_ms": 0.74805, "rwm100_ms": 25.690,
+                        "note": "context, not the target: one 2013 CPU core pair, one chain"}
+    return out
+
+
 def spawn_workers(args, argv):
     """`--gpus N` (N > 1) started as a plain process (no torchrun, WORLD_SIZE unset): re-launch this same command
     under torch.distributed.run with N processes, one per GPU, and return its exit code.  Runs before anything
@@ -284,6 +340,8 @@ def main():
     K, W = args.steps, args.warmup
     burnin = K // 10
     runner = mc.SerialMC(steps=K, burnin=burnin, thinning=args.thinning)
+    if cfg0.get("adapt") and K // 10 >= W + 2:
+        sys.exit("bench.py: the timed run's burnin would reach past the adaptation warmup")
     task = mc.MCMCTask(model, sampler, runner, nchains=C, seed=1, device=local, chain_offset=rank * C,
                        steps_per_launch=max(args.spl, 0))
     h = task.handle()
@@ -304,11 +362,25 @@ def main():
 
     # library-owned output staging sized before the clock starts (the timed run allocates nothing)
     _lib.check(lib.mcmc_chains_reserve_outputs(h, nkept, 0 if args.pcie else 1))
+    adapt = None
     if W > 0:
-        wr = mc.SerialMC(steps=W, burnin=0, thinning=1)
+        # adaptive configs (config 5, HMCDA): the warmup is the configured burnin, W steps of dual averaging
+        # (HMCDA.jl:133: adapts while i < burnin); the timed run continues the same chains (runners.jl:14) past
+        # it, so every timed step runs at the chain's dualLeapStep (HMCDA.jl:140)
+        wr = (mc.SerialMC(steps=W + 1, burnin=W, thinning=1) if cfg0.get("adapt")
+              else mc.SerialMC(steps=W, burnin=0, thinning=1))
         wout = _lib.Outputs()
         cfg = wr.cfg()
+        ta = time.perf_counter()
         _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(wout)))
+        torch.cuda.synchronize(dev)
+        if cfg0.get("adapt"):
+            eps = task.tuner_state()["step_bar"]
+            adapt = {"warmup": f"SerialMC(steps={W + 1}, burnin={W}): {W - 1} dual-averaging updates, untimed",
+                     "warmup_s": time.perf_counter() - ta, "warmup_evals": task.evals,
+                     "eps_bar": {"median": float(np.median(eps)), "min": float(eps.min()), "max": float(eps.max())},
+                     "leapfrogs_per_step_at_eps_bar": {"median": float(np.median(np.maximum(1, np.round(2.0 / eps)))),
+                                                       "max": float(np.max(np.maximum(1, np.round(2.0 / eps))))}}
     torch.cuda.synchronize(dev)
     ev0 = task.evals
     if dist is not None:
@@ -340,8 +412,11 @@ def main():
     if not args.no_ess:
         leg = "timed run"
         e_samples, e_T, e_nkept = samples, T, nkept
-        if nkept < 20:
-            es, eb, et = cfg0["steps"], cfg0["steps"] // 10, cfg0["thinning"]
+        es, eb, et = cfg0["steps"], cfg0["steps"] // 10, cfg0["thinning"]
+        if nkept < 20 and len(mc.SerialMC(steps=es, burnin=eb, thinning=et).r) < 20:
+            leg = f"none: neither the timed run ({nkept}) nor the configuration's SerialMC keeps 20 samples per chain"
+            e_nkept = nkept
+        elif nkept < 20:
             er = mc.SerialMC(steps=es, burnin=eb, thinning=et)
             e_nkept = len(er.r)
             etask = mc.MCMCTask(model, sampler, er, nchains=C, seed=2, device=local, chain_offset=rank * C,
@@ -448,7 +523,7 @@ def main():
                         "note": "SURVEY.md §8(d) bytes of an unfused step (state round trip every step); the "
                                 "fused kernel never moves them, so this rate can exceed HBM peak: it is the north "
                                 "star's '% of HBM roofline' yardstick, not a roofline"}
-        vm = measured_valu(kname)
+        vm = measured_valu(kname, wkey)
         if vm is not None:
             # the binding resource: VALU issue.  SQ_ACTIVE_INST_VALU quad-cycles x 4 = SIMD-cycles of VALU issue
             # per chain-step (measured, committed profile of this kernel instance); achieved = that x chain-steps
@@ -483,6 +558,13 @@ def main():
                 "evals_per_launch": evals / launches,
                 "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
                         "device); 4 n d fp64 flop each (SURVEY.md §8(d))"}
+    # acceptance over the timed run's kept steps (accept bits, SerialMC.jl:55-63)
+    pop8 = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.float64, device=dev)
+    acceptance = float(pop8[bits.view(torch.uint8).long()].sum()) / max(1, nkept * C)
+    if cfg0["model"] != "iso":
+        roof["leapfrogs_per_chain_step" if args.sampler in ("hmc", "hmcda") else "evals_per_chain_step"] = \
+            evals / (C * K)
+        roof["chain_evals_per_s"] = evals * world / T
     line = {
         "metric": "MCMC steps*chains/sec (1M chains, d=32)" if args.config == "metric"
         else f"MCMC steps*chains/sec ({cfg0['desc'].split(':')[0]})",
@@ -507,16 +589,22 @@ def main():
             "parallelism": f"chains sharded over {world} GPU(s), no collective in the step loop",
         },
         "roofline": roof,
+        "acceptance": acceptance,
         "ess": ess_line,
     }
+    if adapt is not None:
+        line["adaptation"] = adapt
+    if args.config == "binomial" and rank == 0:
+        line["reference_units"] = binomial_units(mc, model, C, local)
     if pcie is not None:
         line["pcie_inclusive"] = pcie
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:          # after the timed region, also on N > 1 lines
         line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,
                                             C=min(C, 4096 if cfg0["model"] == "iso" else 64))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
+        dist.barrier()                                  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()
 
 

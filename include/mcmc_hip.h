@@ -183,6 +183,11 @@ int mcmc_chains_destroy(mcmc_chains* chains);
 int mcmc_chains_reset(mcmc_chains* chains);
 /* steps consumed so far (the sampler's own loop counter i). */
 int mcmc_chains_steps_done(mcmc_chains* chains, int64_t* steps);
+/* per-chain adaptive state after the last run, [nchains] each (any may be NULL): step = the current step size
+ * (MALA driftStep under EmpiricalMALATune, HMC leapStep under EmpiricalHMCTune, HMCDA leapStep, HMCDA.jl:136,140);
+ * step_bar = HMCDA's dual-averaged dualLeapStep (HMCDA.jl:138); nleaps = the tuned HMC nLeaps (HMC.jl:42).
+ * A quantity the sampler does not adapt reads NaN (steps) or 0 (nleaps). */
+int mcmc_chains_tuner_state(mcmc_chains* chains, double* step, double* step_bar, int32_t* nleaps);
 /* log-target evaluations (with gradient for MALA/HMC/HMCDA) summed over all chains since
  * create/reset: steps x C for RWM/MALA, the leapfrog count for HMC/HMCDA (HMC.jl:93-102),
  * whose trajectory length varies per chain under HMCDA / EmpMCTuner. */
@@ -254,9 +259,15 @@ int mcmc_group_chains_block(mcmc_group_chains* gc, int32_t g, mcmc_chains** chai
                             int64_t* count);
 /* run_serialmc on every block concurrently; out holds host buffers for all nchains chains (mcmc_outputs
  * layout); out->runtime_s / kernel_ms: the slowest block's step loop; gather_s (may be NULL): the slowest
- * block's device -> host gather of its outputs. */
+ * block's device -> host gather of its outputs.  Output buffers that are not already page-locked are
+ * registered (hipHostRegister, portable) for the duration of the call, so the gather is direct DMA; callers
+ * that run repeatedly into the same buffers can pin them once themselves.  If any block fails, the error
+ * names the block and device, and these chains refuse further runs (and steps_done) until
+ * mcmc_group_chains_reset: the blocks may then be at different steps. */
 int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_cfg* runner, mcmc_outputs* out,
                             double* gather_s);
+/* test hook: the next mcmc_group_run_serialmc fails block `block` before it starts (the others run) */
+int mcmc_debug_group_inject_failure(mcmc_group_chains* gc, int32_t block);
 
 /* ---- SeqMC population runner (src/runners/SeqMC.jl:21-122) ----
  * targets[t] (t < ntargets) are chain batches of one context, equal d, each with nchains == npart:

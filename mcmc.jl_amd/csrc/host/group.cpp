@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -29,9 +30,19 @@ struct mcmc_group_chains {
     std::vector<int64_t> first, count;
     std::vector<mcmc_model*> model;  // per block (NULL for an empty block)
     std::vector<mcmc_chains*> chains;
+    // a run in which some block failed leaves the blocks at different steps: every later run is refused
+    // until mcmc_group_chains_reset puts all blocks back at model.init (the bit-identity with one context
+    // would otherwise be lost silently)
+    bool failed = false;
+    std::string fail_msg;
+    int32_t inject_fail = -1;        // mcmc_debug_group_inject_failure: this block's next run fails before it starts
 };
 
 static int bad(const char* msg) { return mcmc_set_error(MCMC_E_INVALID_ARG, msg); }
+
+static int64_t kept_rows(const mcmc_runner_cfg& r) {        // length of (burnin+1):thinning:len
+    return r.len <= r.burnin ? 0 : (r.len - r.burnin - 1) / r.thinning + 1;
+}
 
 extern "C" int mcmc_group_plan(int64_t nchains, int32_t nblocks, int64_t* first, int64_t* count) {
     if (nchains <= 0 || nblocks <= 0 || !first || !count) return bad("bad argument");
@@ -141,15 +152,27 @@ extern "C" int mcmc_group_chains_reset(mcmc_group_chains* gc) {
     if (!gc) return bad("NULL argument");
     for (mcmc_chains* c : gc->chains)
         if (c)
-            if (int rc = mcmc_chains_reset(c)) return rc;
+            if (int rc = mcmc_chains_reset(c)) return rc;       // still failed: a block kept its old state
+    gc->failed = false;
+    gc->fail_msg.clear();
     return MCMC_OK;
 }
 
 extern "C" int mcmc_group_chains_steps_done(mcmc_group_chains* gc, int64_t* steps) {
     if (!gc || !steps) return bad("NULL argument");
-    for (mcmc_chains* c : gc->chains)
-        if (c) return mcmc_chains_steps_done(c, steps);          // every block has run the same steps
-    return bad("no chains");
+    int64_t s0 = -1;
+    for (mcmc_chains* c : gc->chains) {
+        if (!c) continue;
+        int64_t s = 0;
+        if (int rc = mcmc_chains_steps_done(c, &s)) return rc;
+        if (s0 >= 0 && s != s0)
+            return mcmc_set_error(MCMC_E_INVALID_ARG, "mcmc_group_chains_steps_done: the blocks are at different "
+                                                      "steps (a failed run); mcmc_group_chains_reset first");
+        s0 = s;
+    }
+    if (s0 < 0) return bad("no chains");
+    *steps = s0;
+    return MCMC_OK;
 }
 
 extern "C" int mcmc_group_chains_set_steps_per_launch(mcmc_group_chains* gc, int64_t spl) {
@@ -169,11 +192,33 @@ extern "C" int mcmc_group_chains_block(mcmc_group_chains* gc, int32_t b, mcmc_ch
     return MCMC_OK;
 }
 
+// The caller's host output buffers, page-locked for the gather: a buffer that is not already pinned is
+// registered (portable: visible to every device's copy engine) for the duration of the run and released after
+// it.  Device -> host copies into pageable memory are staged through a driver bounce buffer at a fraction of
+// the link rate; into pinned memory they are direct DMA.
+struct PinnedOutputs {
+    std::vector<void*> registered;
+    double reg_s = 0.0;
+    void pin(void* p, size_t bytes) {
+        if (!p || bytes == 0) return;
+        const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+        if (e == hipSuccess) registered.push_back(p);
+        else (void)hipGetLastError();           // already pinned (hipErrorHostMemoryAlreadyRegistered) or not
+                                                // registrable: the copy still works, staged
+    }
+    ~PinnedOutputs() {
+        for (void* p : registered) (void)hipHostUnregister(p);
+    }
+};
+
 extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_cfg* r, mcmc_outputs* out,
                                        double* gather_s) {
     if (!gc || !r) return bad("NULL argument");
     if (int rc = mcmc_runner_validate(r)) return rc;
     if (out && out->on_device) return bad("group runs write host buffers (on_device must be 0)");
+    if (gc->failed)
+        return mcmc_set_error(MCMC_E_INVALID_ARG, "mcmc_group_run_serialmc: an earlier run of these chains failed (" +
+                                                      gc->fail_msg + "); mcmc_group_chains_reset first");
     const int32_t G = (int32_t)gc->chains.size();
     const int64_t C = gc->C;
     struct Res {
@@ -183,6 +228,17 @@ extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_
         double copy_s = 0.0;
     };
     std::vector<Res> res(G);
+    PinnedOutputs pins;
+    if (out) {
+        const size_t nk = (size_t)kept_rows(*r), d = (size_t)gc->d, nw = (size_t)(C + 63) / 64;
+        auto c0 = std::chrono::steady_clock::now();
+        pins.pin(out->samples, nk * d * (size_t)C * 8);
+        pins.pin(out->gradients, nk * d * (size_t)C * 8);
+        pins.pin(out->accept_bits, nk * nw * 8);
+        pins.pin(out->final_x, d * (size_t)C * 8);
+        pins.pin(out->final_lp, (size_t)C * 8);
+        pins.reg_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+    }
     auto work = [&](int32_t b) {
         Res& R = res[b];
         mcmc_outputs* po = nullptr;
@@ -196,25 +252,43 @@ extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_
             R.o.on_device = 0;
             po = &R.o;
         }
+        if (b == gc->inject_fail) {
+            R.rc = MCMC_E_HIP;
+            R.msg = "injected failure (mcmc_debug_group_inject_failure)";
+            return;
+        }
         R.rc = mcmc_run_serialmc_ld(gc->chains[b], r, po, C, &R.copy_s);
         if (R.rc) R.msg = mcmc_last_error();                     // the worker's thread-local message
     };
-    std::vector<std::thread> th;
-    int32_t last = -1;
+    std::vector<int32_t> blocks;
     for (int32_t b = 0; b < G; ++b)
-        if (gc->chains[b]) {
-            if (last >= 0) th.emplace_back(work, last);
-            last = b;
-        }
-    if (last < 0) return bad("no chains");
-    work(last);                                                  // the calling thread drives one block itself
-    for (auto& t : th) t.join();
+        if (gc->chains[b]) blocks.push_back(b);
+    if (blocks.empty()) return bad("no chains");
+    std::vector<std::thread> th;
+    bool spawn_failed = false;
+    try {
+        for (size_t i = 0; i + 1 < blocks.size(); ++i) th.emplace_back(work, blocks[i]);
+    } catch (...) {                                              // std::system_error: no thread could be started
+        spawn_failed = true;
+    }
+    if (!spawn_failed) work(blocks.back());                      // the calling thread drives one block itself
+    for (auto& t : th) t.join();                                 // every started worker, also after a failure
+    gc->inject_fail = -1;
+    if (spawn_failed) {
+        // blocks whose worker started have advanced; the others have not
+        gc->failed = true;
+        gc->fail_msg = "could not start a worker thread";
+        return mcmc_set_error(MCMC_E_HIP, "mcmc_group_run_serialmc: could not start a worker thread");
+    }
     double rt = 0.0, kms = 0.0, gs = 0.0;
-    for (int32_t b = 0; b < G; ++b) {
-        if (!gc->chains[b]) continue;
-        if (res[b].rc)
-            return mcmc_set_error(res[b].rc, "block " + std::to_string(b) + " (device " +
-                                                  std::to_string(gc->group->devices[b]) + "): " + res[b].msg);
+    for (int32_t b : blocks) {
+        if (res[b].rc) {
+            const std::string msg = "block " + std::to_string(b) + " (device " +
+                                    std::to_string(gc->group->devices[b]) + "): " + res[b].msg;
+            gc->failed = true;
+            gc->fail_msg = msg;
+            return mcmc_set_error(res[b].rc, msg);
+        }
         rt = std::max(rt, res[b].o.runtime_s);
         kms = std::max(kms, res[b].o.kernel_ms);
         gs = std::max(gs, res[b].copy_s);
@@ -222,8 +296,14 @@ extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_
     if (out) {
         out->runtime_s = rt;
         out->kernel_ms = kms;
-        out->nkept = res[last].o.nkept;
+        out->nkept = res[blocks.back()].o.nkept;
     }
     if (gather_s) *gather_s = gs;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_debug_group_inject_failure(mcmc_group_chains* gc, int32_t block) {
+    if (!gc || block < 0 || block >= (int32_t)gc->chains.size()) return bad("bad block index");
+    gc->inject_fail = block;
     return MCMC_OK;
 }

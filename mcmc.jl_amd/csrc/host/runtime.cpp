@@ -775,6 +775,33 @@ extern "C" int mcmc_chains_ram_factor(mcmc_chains* c, double* S) {
     return MCMC_OK;
 }
 
+// per-chain adaptive state: the step size (MALA driftStep, HMC leapStep, HMCDA leapStep), HMCDA's dual-averaged
+// step (dualLeapStep, HMCDA.jl:139) and the tuned HMC nLeaps; a buffer the sampler does not keep is filled with
+// NaN (step, step_bar) or 0 (nleaps)
+extern "C" int mcmc_chains_tuner_state(mcmc_chains* c, double* step, double* step_bar, int32_t* nleaps) {
+    if (!c) return fail(MCMC_E_INVALID_ARG, "chains is NULL");
+    mcmc_ctx* ctx = c->model->ctx;
+    if (int r = set_device(ctx)) return r;
+    const size_t C = (size_t)c->C;
+    auto get = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+        return e == hipSuccess ? hipStreamSynchronize(ctx->stream) : e;
+    };
+    if (step) {
+        if (c->st.t_step) HIP_TRY(get(step, c->st.t_step, C * 8));
+        else std::fill(step, step + C, __builtin_nan(""));
+    }
+    if (step_bar) {
+        if (c->st.t_bar) HIP_TRY(get(step_bar, c->st.t_bar, C * 8));
+        else std::fill(step_bar, step_bar + C, __builtin_nan(""));
+    }
+    if (nleaps) {
+        if (c->st.t_leaps) HIP_TRY(get(nleaps, c->st.t_leaps, C * 4));
+        else std::fill(nleaps, nleaps + C, 0);
+    }
+    return MCMC_OK;
+}
+
 extern "C" int mcmc_chains_steps_done(mcmc_chains* c, int64_t* steps) {
     if (!c || !steps) return fail(MCMC_E_INVALID_ARG, "NULL argument");
     *steps = c->steps_done;

@@ -7,9 +7,12 @@
 
 namespace mcmc {
 
+#ifndef LPC_MINW
+#define LPC_MINW 2
+#endif
 // F: d == 4 NB (LaneChain FULL); US: uniform RWM scale
 template <int NB, bool F, class M, bool US>
-__global__ __launch_bounds__(kBlock, 2) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
+__global__ __launch_bounds__(kBlock, LPC_MINW) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
 template <int NB, bool F, class M>
 __global__ __launch_bounds__(kBlock, 2) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
 template <int NB, bool F, class M, bool DA>
@@ -18,6 +21,22 @@ template <int NB, class M>
 __global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {
     eval_body<LaneChain<NB>, M>(a, xin, lp, g, check);
+}
+
+// 16 < d <= 32: two lanes per chain (samplers.hpp PairChain), NB Philox blocks per lane; four waves per SIMD
+// Waves per SIMD (the launch bound): RWM holds x and the proposal, 16 coordinates each, in 128 VGPRs (4 waves; 3
+// when d < 2 NC leaves per-coordinate masks live); MALA 3 (2 with masks); HMC's x0, x, momentum and carried kicks
+// need ~240 (2 waves, where the lane-per-chain d = 32 kernel fitted one)
+template <int NB, bool F, class M, bool US>
+__global__ __launch_bounds__(kBlock, F && US ? 4 : 3) void lpp_rwm(KernelArgs a) { rwm_body<PairChain<NB, F>, M, US>(a); }
+template <int NB, bool F, class M>
+__global__ __launch_bounds__(kBlock, F ? 3 : 2) void lpp_mala(KernelArgs a) { mala_body<PairChain<NB, F>, M>(a); }
+template <int NB, bool F, class M, bool DA>
+__global__ __launch_bounds__(kBlock, 2) void lpp_hmc(KernelArgs a) { hmc_body<PairChain<NB, F>, M, DA>(a); }
+template <int NB, class M>
+__global__ __launch_bounds__(kBlock) void lpp_eval(KernelArgs a, const double* xin, double* lp, double* g,
+                                                   int32_t check) {
+    eval_body<PairChain<NB>, M>(a, xin, lp, g, check);
 }
 
 // RWM for a handful of chains (C <= 64; config 1 is one chain), where one lane per chain leaves the chip idle
@@ -31,7 +50,7 @@ constexpr int kLaMaxChains = 64;
 constexpr int kLaGen = kBlock - 64;                  // generating threads
 template <int NB, class M, bool US>
 __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
-    using P = LaneChain<NB, false>;
+    using P = LaneChain<NB, false, (NB > 4)>;        // d > 16: PairChain's summation order (lpp_rwm's chains)
     constexpr int NC = P::NC;
     const StepArgs& s = a.s;
     const P p(s);                                    // stages the Box-Muller tables (every thread)
@@ -297,46 +316,83 @@ static void lpc_spec_launch(const KernelArgs& a, hipStream_t st) {
     else lpc_rwm_spec<D, M, false><<<1, kBlock, 0, st>>>(a);
 }
 
-template <int NB, bool F, class M>
-static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
-    const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+// 16 < d <= 32 (NB = ceil(d/4) > 4): the two-lanes-per-chain kernels, NBL = ceil(NB / 2) blocks per lane
+template <int NBL, bool F, class M>
+static hipError_t lpp_launch(const KernelArgs& a, hipStream_t st) {
+    const dim3 grid((unsigned)((a.s.C + PairChain<NBL>::kChainsPerBlock - 1) / PairChain<NBL>::kChainsPerBlock));
     const char* b = F ? "true" : "false";
     const char* us = a.s.scale_uniform ? "true" : "false";
     switch (a.sa.kind) {
         case SK_RWM:
-            if (NB == 1 && a.s.C == 1) {
-                mcmc_note_step_kernel("lpc_rwm_spec<%d, %s, %s>", (int)a.s.d, M::kName, us);
-                switch (a.s.d) {
-                    case 1: lpc_spec_launch<1, M>(a, st); break;
-                    case 2: lpc_spec_launch<2, M>(a, st); break;
-                    case 3: lpc_spec_launch<3, M>(a, st); break;
-                    default: lpc_spec_launch<4, M>(a, st); break;
-                }
-                break;
-            }
-            if (a.s.C <= kLaMaxChains) {
-                mcmc_note_step_kernel("lpc_rwm_la<%d, %s, %s>", NB, M::kName, us);
-                if (a.s.scale_uniform) lpc_rwm_la<NB, M, true><<<1, kBlock, 0, st>>>(a);
-                else lpc_rwm_la<NB, M, false><<<1, kBlock, 0, st>>>(a);
-                break;
-            }
-            mcmc_note_step_kernel("lpc_rwm<%d, %s, %s, %s>", NB, b, M::kName, us);
-            if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
-            else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            mcmc_note_step_kernel("lpp_rwm<%d, %s, %s, %s>", NBL, b, M::kName, us);
+            if (a.s.scale_uniform) lpp_rwm<NBL, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            else lpp_rwm<NBL, F, M, false><<<grid, kBlock, 0, st>>>(a);
             break;
         case SK_MALA:
-            mcmc_note_step_kernel("lpc_mala<%d, %s, %s>", NB, b, M::kName);
-            lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a);
+            mcmc_note_step_kernel("lpp_mala<%d, %s, %s>", NBL, b, M::kName);
+            lpp_mala<NBL, F, M><<<grid, kBlock, 0, st>>>(a);
             break;
         case SK_HMC:
-            mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, false>", NB, b, M::kName);
-            lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            mcmc_note_step_kernel("lpp_hmc<%d, %s, %s, false>", NBL, b, M::kName);
+            lpp_hmc<NBL, F, M, false><<<grid, kBlock, 0, st>>>(a);
             break;
         case SK_HMCDA:
-            mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, true>", NB, b, M::kName);
-            lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            mcmc_note_step_kernel("lpp_hmc<%d, %s, %s, true>", NBL, b, M::kName);
+            lpp_hmc<NBL, F, M, true><<<grid, kBlock, 0, st>>>(a);
             break;
         default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int NB, bool F, class M>
+static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
+    const char* us = a.s.scale_uniform ? "true" : "false";
+    const bool few = a.sa.kind == SK_RWM && a.s.C <= kLaMaxChains;      // lpc_rwm_la (split order for d > 16)
+    if constexpr (NB > 4) {
+        if (!few) return lpp_launch<(NB + 1) / 2, F && (NB % 2 == 0), M>(a, st);
+        mcmc_note_step_kernel("lpc_rwm_la<%d, %s, %s>", NB, M::kName, us);
+        if (a.s.scale_uniform) lpc_rwm_la<NB, M, true><<<1, kBlock, 0, st>>>(a);
+        else lpc_rwm_la<NB, M, false><<<1, kBlock, 0, st>>>(a);
+    } else {
+        const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+        const char* b = F ? "true" : "false";
+        switch (a.sa.kind) {
+            case SK_RWM:
+                if (NB == 1 && a.s.C == 1) {
+                    mcmc_note_step_kernel("lpc_rwm_spec<%d, %s, %s>", (int)a.s.d, M::kName, us);
+                    switch (a.s.d) {
+                        case 1: lpc_spec_launch<1, M>(a, st); break;
+                        case 2: lpc_spec_launch<2, M>(a, st); break;
+                        case 3: lpc_spec_launch<3, M>(a, st); break;
+                        default: lpc_spec_launch<4, M>(a, st); break;
+                    }
+                    break;
+                }
+                if (a.s.C <= kLaMaxChains) {
+                    mcmc_note_step_kernel("lpc_rwm_la<%d, %s, %s>", NB, M::kName, us);
+                    if (a.s.scale_uniform) lpc_rwm_la<NB, M, true><<<1, kBlock, 0, st>>>(a);
+                    else lpc_rwm_la<NB, M, false><<<1, kBlock, 0, st>>>(a);
+                    break;
+                }
+                mcmc_note_step_kernel("lpc_rwm<%d, %s, %s, %s>", NB, b, M::kName, us);
+                if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+                else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+                break;
+            case SK_MALA:
+                mcmc_note_step_kernel("lpc_mala<%d, %s, %s>", NB, b, M::kName);
+                lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a);
+                break;
+            case SK_HMC:
+                mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, false>", NB, b, M::kName);
+                lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+                break;
+            case SK_HMCDA:
+                mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, true>", NB, b, M::kName);
+                lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+                break;
+            default: return hipErrorInvalidValue;
+        }
     }
     return hipGetLastError();
 }
@@ -367,15 +423,16 @@ template <class M>
 static hipError_t lpc_eval_m(const KernelArgs& a, const double* xin, double* lp, double* g, int check,
                              hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    const dim3 grid2((unsigned)((a.s.C + kBlock / 2 - 1) / (kBlock / 2)));       // PairChain: 128 chains a block
     switch ((a.s.d + 3) / 4) {
         case 1: lpc_eval<1, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
         case 2: lpc_eval<2, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
         case 3: lpc_eval<3, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
         case 4: lpc_eval<4, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
-        case 5: lpc_eval<5, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
-        case 6: lpc_eval<6, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
-        case 7: lpc_eval<7, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
-        case 8: lpc_eval<8, M><<<grid, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 5:
+        case 6: lpp_eval<3, M><<<grid2, kBlock, 0, st>>>(a, xin, lp, g, check); break;
+        case 7:
+        case 8: lpp_eval<4, M><<<grid2, kBlock, 0, st>>>(a, xin, lp, g, check); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -385,20 +442,30 @@ static hipError_t lpc_eval_m(const KernelArgs& a, const double* xin, double* lp,
 template <int NB, class M, bool DA>
 __global__ __launch_bounds__(kBlock) void lpc_hmc_rec(KernelArgs a, LeapRec r) { hmc_record_body<LaneChain<NB>, M, DA>(a, r); }
 
+template <int NB, class M, bool DA>
+__global__ __launch_bounds__(kBlock) void lpp_hmc_rec(KernelArgs a, LeapRec r) { hmc_record_body<PairChain<NB>, M, DA>(a, r); }
+
 template <class M>
 static hipError_t lpc_record_m(const KernelArgs& a, const LeapRec& r, hipStream_t st) {
     const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+    const dim3 grid2((unsigned)((a.s.C + kBlock / 2 - 1) / (kBlock / 2)));
     const bool da = a.sa.kind == SK_HMCDA;
 #define LPC_REC(NB)                                                       \
     case NB:                                                              \
         if (da) lpc_hmc_rec<NB, M, true><<<grid, kBlock, 0, st>>>(a, r);   \
         else lpc_hmc_rec<NB, M, false><<<grid, kBlock, 0, st>>>(a, r);     \
         break;
+#define LPP_REC(NB, NBL)                                                    \
+    case NB:                                                                \
+        if (da) lpp_hmc_rec<NBL, M, true><<<grid2, kBlock, 0, st>>>(a, r);   \
+        else lpp_hmc_rec<NBL, M, false><<<grid2, kBlock, 0, st>>>(a, r);     \
+        break;
     switch ((a.s.d + 3) / 4) {
-        LPC_REC(1) LPC_REC(2) LPC_REC(3) LPC_REC(4) LPC_REC(5) LPC_REC(6) LPC_REC(7) LPC_REC(8)
+        LPC_REC(1) LPC_REC(2) LPC_REC(3) LPC_REC(4) LPP_REC(5, 3) LPP_REC(6, 3) LPP_REC(7, 4) LPP_REC(8, 4)
         default: return hipErrorInvalidValue;
     }
 #undef LPC_REC
+#undef LPP_REC
     return hipGetLastError();
 }
 

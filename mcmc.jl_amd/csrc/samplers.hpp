@@ -67,10 +67,15 @@ __device__ __forceinline__ void bm_lds_tables(const double (*&lt)[4], const doub
 // ------------------------------------------------------------------ mappings
 // NB = ceil(d/4).  FULL: d == 4 NB, every register coordinate is a real one -- no validity masks
 // (with a runtime d they are per-coordinate uniform masks, which overflow the SGPR file at NB = 8).
-template <int NB_, bool FULL = false>
+// SPLIT: eval_lp sums in PairChain's order (coordinates of the first PairChain half, then the second, then the two
+// partial sums added) -- for the few-chain RWM kernel lpc_rwm_la, which runs the same chains as the 16 < d <= 32
+// PairChain kernels and must agree with them bit for bit
+template <int NB_, bool FULL = false, bool SPLIT = false>
 struct LaneChain {
     static constexpr int NB = NB_;
     static constexpr int NC = 4 * NB_;
+    static constexpr int kSplit = SPLIT ? 4 * ((NB_ + 1) / 2) : 0;
+    static constexpr int kChainsPerBlock = kBlock;
     int64_t c;        // local chain index
     bool live;        // c < C
     int d;
@@ -152,6 +157,113 @@ struct LaneChain {
         if ((threadIdx.x & 63) == 0 && s.acc_bits != nullptr) {
             const int64_t w = c >> 6;
             if (w < s.nw) s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)w] = mask;
+        }
+    }
+};
+
+// Two lanes per chain (16 < d <= 32): lane l of a wave holds half h = l >> 5 of chain (l & 31) of the wave's 32
+// chains -- coordinates h NC .. h NC + NC - 1 (NC = 4 NB, NB = ceil(ceil(d/4) / 2) Philox blocks per lane) -- so a
+// lane carries half the state and proposal of LaneChain and the kernel fits four waves per SIMD instead of two
+// (the VALU issue rate of a SIMD grows with the waves it can pick from; scripts/probe_valu_rates.hip).  Sums: each
+// lane accumulates its coordinates left to right, then (half 0) + (half 1), formed identically in both lanes by
+// one v_permlane32_swap per dword (oracle order ORC_ORDER_PAIR).  Both lanes of a chain hold the same lp, ratio
+// and accept decision; memory: row k of the wave's 32 chains is one 256-byte run per half.
+template <int NB_, bool FULL = false>
+struct PairChain {
+    static constexpr int NB = NB_;
+    static constexpr int NC = 4 * NB_;
+    static constexpr int kChainsPerBlock = kBlock / 2;
+    int64_t c;        // local chain index
+    bool live;
+    int d;
+    int h;            // half: 0 (lanes 0-31) or 1 (lanes 32-63)
+    const double (*tab)[4];
+    const double (*sct)[2];
+    __device__ PairChain(const StepArgs& s, bool defer = false) {
+        const int lane = (int)(threadIdx.x & 63);
+        c = (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)(threadIdx.x >> 6) * 32 + (lane & 31);
+        h = lane >> 5;
+        live = c < s.C;
+        d = s.d;
+        bm_lds_tables(tab, sct);
+        if (!defer) stage();
+    }
+    __device__ __forceinline__ void stage() const { stage_bm_tables(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct)); }
+    __device__ __forceinline__ int coord(int k) const { return h * NC + k; }
+    __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
+    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(h * NB + b); }
+    // (half 0's value) + (half 1's value) in both lanes of the chain, bitwise the same
+    __device__ __forceinline__ double reduce(double v) const {
+        const uint64_t u = (uint64_t)__double_as_longlong(v);
+        const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);   // {half 0's, half 1's}
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        const double v0 = __longlong_as_double((long long)(((uint64_t)b[0] << 32) | a[0]));
+        const double v1 = __longlong_as_double((long long)(((uint64_t)b[1] << 32) | a[1]));
+        return v0 + v1;
+    }
+    __device__ __forceinline__ bool any(bool v) const {
+        const uint64_t m = __ballot(v);
+        const int l = (int)(threadIdx.x & 31);
+        return (((m >> l) | (m >> (l + 32))) & 1ull) != 0;
+    }
+    __device__ __forceinline__ void load(const double* x, int64_t ld, double (&v)[NC]) const {
+        uint64_t o = (uint64_t)(live ? c : 0) + (uint64_t)(h * NC) * (uint64_t)ld;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            v[k] = valid(k) ? x[o] : 0.0;
+            o += (uint64_t)ld;
+            asm volatile("" : "+v"(o));
+        }
+    }
+    __device__ __forceinline__ void store(double* x, int64_t ld, const double (&v)[NC]) const {
+        if (!live) return;
+        uint64_t o = (uint64_t)c + (uint64_t)(h * NC) * (uint64_t)ld;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (valid(k)) x[o] = v[k];
+            o += (uint64_t)ld;
+            asm volatile("" : "+v"(o));
+        }
+    }
+    __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ T load_t(const T* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ void store_t(T* p, T v) const {
+        if (live && h == 0) p[c] = v;
+    }
+    __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
+                                               double* base) const {
+        if (base == nullptr || !live) return;
+        double* p = base + (size_t)kk * (size_t)d * (size_t)s.C;
+        const uint64_t C = (uint64_t)s.C;
+        uint64_t o = (uint64_t)c + (uint64_t)(h * NC) * C;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (valid(k)) p[o] = v[k];
+            o += C;
+            asm volatile("" : "+v"(o));
+        }
+    }
+    __device__ __forceinline__ void store_cm(const StepArgs& s, int64_t l, const double (&v)[NC], double* base) const {
+        store_kept(s, l, v, base);
+    }
+    __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
+        if (s.n_evals == nullptr) return;
+        unsigned long long v = (live && h == 0) ? (unsigned long long)n : 0ull;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(s.n_evals, v);
+    }
+    // the wave's 32 chains are one half-word of an accept-bit word (bit c % 64 of word c / 64, little-endian)
+    __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
+        const uint64_t mask = __ballot(acc && live);
+        if ((threadIdx.x & 63) == 0 && s.acc_bits != nullptr) {
+            const int64_t w = c >> 6;
+            if (w < s.nw)
+                reinterpret_cast<uint32_t*>(s.acc_bits)[((size_t)kk * (size_t)s.nw + (size_t)w) * 2 + (size_t)((c >> 5) & 1)] =
+                    (uint32_t)mask;
         }
     }
 };
@@ -286,8 +398,24 @@ __device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32
     }
 }
 
+template <class P>
+struct split_of { static constexpr int value = 0; };
+template <int NB, bool F, bool S>
+struct split_of<LaneChain<NB, F, S>> { static constexpr int value = LaneChain<NB, F, S>::kSplit; };
+
 template <class P, class M>
 __device__ __forceinline__ double eval_lp(const P& p, const M& model, const double (&v)[P::NC], bool& oos) {
+    constexpr int S = split_of<P>::value;
+    if constexpr (S > 0) {                              // LaneChain SPLIT: PairChain's order (see LaneChain)
+        double a = 0.0, b = 0.0;
+#pragma unroll
+        for (int k = 0; k < P::NC; ++k)
+            if (p.valid(k)) {
+                if (k < S) model.acc(a, v[k]);
+                else model.acc(b, v[k]);
+            }
+        return llacc_finish(model, a + b, oos);
+    }
     double a = 0.0;
 #pragma unroll
     for (int k = 0; k < P::NC; ++k)

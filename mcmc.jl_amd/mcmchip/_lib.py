@@ -48,12 +48,13 @@ EXPORTED_SYMBOLS = (
     "mcmc_model_create", "mcmc_model_destroy", "mcmc_model_eval",
     "mcmc_sampler_validate", "mcmc_runner_validate",
     "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done", "mcmc_chains_evals",
-    "mcmc_chains_ram_factor",
+    "mcmc_chains_ram_factor", "mcmc_chains_tuner_state",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients", "mcmc_chains_reserve_outputs",
     "mcmc_chains_launches", "mcmc_chains_step_kernel", "mcmc_chains_store_leaps", "mcmc_run_serialmc",
     "mcmc_group_create", "mcmc_group_destroy", "mcmc_group_size", "mcmc_group_plan", "mcmc_group_chains_create",
     "mcmc_group_chains_destroy", "mcmc_group_chains_reset", "mcmc_group_chains_steps_done",
     "mcmc_group_chains_set_steps_per_launch", "mcmc_group_chains_block", "mcmc_group_run_serialmc",
+    "mcmc_debug_group_inject_failure",
     "mcmc_seqmc_validate", "mcmc_run_seqmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox",
     "mcmc_debug_mfma_f64",
 )
@@ -146,6 +147,7 @@ def load() -> ct.CDLL:
         "mcmc_chains_steps_done": (ct.c_int, [P, ct.POINTER(i64)]),
         "mcmc_chains_evals": (ct.c_int, [P, ct.POINTER(i64)]),
         "mcmc_chains_ram_factor": (ct.c_int, [P, ct.c_void_p]),
+        "mcmc_chains_tuner_state": (ct.c_int, [P, ct.c_void_p, ct.c_void_p, ct.c_void_p]),
         "mcmc_chains_set_steps_per_launch": (ct.c_int, [P, i64]),
         "mcmc_chains_set_store_gradients": (ct.c_int, [P, i32]),
         "mcmc_chains_reserve_outputs": (ct.c_int, [P, i64, i32]),
@@ -167,6 +169,7 @@ def load() -> ct.CDLL:
         "mcmc_group_chains_block": (ct.c_int, [P, i32, pp, ct.POINTER(i64), ct.POINTER(i64)]),
         "mcmc_group_run_serialmc": (ct.c_int, [P, ct.POINTER(RunnerCfg), ct.POINTER(Outputs),
                                                ct.POINTER(ct.c_double)]),
+        "mcmc_debug_group_inject_failure": (ct.c_int, [P, i32]),
         "mcmc_seqmc_validate": (ct.c_int, [ct.c_void_p]),
         "mcmc_run_seqmc": (ct.c_int, [ct.POINTER(ct.c_void_p), i32, i64, ct.c_void_p, ct.c_void_p, u64, i32,
                                       ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.POINTER(ct.c_double)]),

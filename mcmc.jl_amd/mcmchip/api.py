@@ -552,6 +552,22 @@ class MCMCTask:
                 tot += v.value
         return tot
 
+    def tuner_state(self):
+        """Per-chain adaptive state after the last run (mcmc_chains_tuner_state): a dict of [nchains] arrays
+        "step" (MALA driftStep / HMC leapStep under the empirical tuners; HMCDA leapStep), "step_bar" (HMCDA's
+        dualLeapStep, HMCDA.jl:138) and "nleaps" (tuned HMC); NaN / 0 where the sampler does not adapt it."""
+        C = self.nchains
+        step = np.empty(C)
+        bar = np.empty(C)
+        nl = np.empty(C, dtype=np.int32)
+        for c, f, n in self.blocks():
+            if c is None:
+                continue
+            a, b, k = np.empty(n), np.empty(n), np.empty(n, dtype=np.int32)
+            check(_lib.load().mcmc_chains_tuner_state(c, a.ctypes.data, b.ctypes.data, k.ctypes.data))
+            step[f:f + n], bar[f:f + n], nl[f:f + n] = a, b, k
+        return {"step": step, "step_bar": bar, "nleaps": nl}
+
     @property
     def step_kernel(self) -> str:
         """The step kernel instance the last run launched (mcmc_chains_step_kernel), e.g.

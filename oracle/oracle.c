@@ -17,7 +17,8 @@
  * build's specification: sums left to right over coordinates
  * (order 0, lane-per-chain kernels) or per-lane partials + xor butterfly over 64
  * lanes (order 1, wave-per-chain kernels); order W > 1: a chain spread over W waves (lane l of 64 W owns
- * 4 (l + 64 W k) + e), each wave's butterfly, then the W wave sums left to right (block-per-chain kernels).
+ * 4 (l + 64 W k) + e), each wave's butterfly, then the W wave sums left to right (block-per-chain kernels);
+ * order ORC_ORDER_PAIR (-2): two lanes per chain (16 < d <= 32), each half left to right, then the halves added.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -82,6 +83,7 @@ static const double ORC_LOG2PI = 0x1.d67f1c864beb5p+0;
 static const double ORC_TWOPI = 0x1.921fb54442d18p+2;
 
 /* ------------------------------------------------------------ reductions */
+#define ORC_ORDER_PAIR (-2)
 /* order 1: lane l of a 64-lane wave owns coordinates 4*(l + 64k) + e, e = 0..3, k = 0,1,...;
    each lane accumulates its coordinates in (k, e) order, then xor butterfly 32,16,...,1.
    order W > 1: lane l of 64 W owns 4*(l + 64 W k) + e; butterfly per wave, wave sums left to right. */
@@ -100,11 +102,22 @@ static double orc_glm_sum(const double* t, const orc_glm_geo* g, int d, int fuse
 
 static int orc_is_glm(const orc_model* m) { return m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR; }
 
+/* order ORC_ORDER_PAIR (16 < d <= 32, two lanes per chain, samplers.hpp PairChain): the first S = 4 ceil(ceil(d/4)/2)
+   coordinates left to right, the rest left to right, then (first) + (second) */
+static int orc_pair_split(int d) { return 4 * (((d + 3) / 4 + 1) / 2); }
+
 static double orc_dot(const double* v, const orc_model* mdl, int order) {
     const int d = mdl->d;
     if (orc_is_glm(mdl)) {
         orc_glm_geo geo = orc_glm_geometry(mdl);
         return orc_glm_sum(v, &geo, d, 1);
+    }
+    if (order == ORC_ORDER_PAIR) {
+        const int S = orc_pair_split(d);
+        double a = 0.0, b = 0.0;
+        for (int j = 0; j < d && j < S; ++j) a = fma(v[j], v[j], a);
+        for (int j = S; j < d; ++j) b = fma(v[j], v[j], b);
+        return a + b;
     }
     if (order == 0) {
         double a = 0.0;
@@ -132,6 +145,13 @@ static double orc_sum(const double* t, const orc_model* mdl, int order) {
     if (orc_is_glm(mdl)) {
         orc_glm_geo geo = orc_glm_geometry(mdl);
         return orc_glm_sum(t, &geo, d, 0);
+    }
+    if (order == ORC_ORDER_PAIR) {
+        const int S = orc_pair_split(d);
+        double a = 0.0, b = 0.0;
+        for (int j = 0; j < d && j < S; ++j) a = a + t[j];
+        for (int j = S; j < d; ++j) b = b + t[j];
+        return a + b;
     }
     if (order == 0) {
         double a = 0.0;

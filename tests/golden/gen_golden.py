@@ -98,9 +98,10 @@ def case_sampler(spec, sname):
 
 
 def order_for(spec):
-    """lane-per-chain kernels (d <= 32) sum left to right; wave-per-chain kernels per lane + butterfly;
-    regression kernels have their own fixed order (the oracle picks it from the model)."""
-    return 0 if spec["d"] <= 32 or spec["model"] in ("logistic", "linear") else 1
+    """None: the library's own summation order for the model / sampler (oracle_ref.kernel_order): lane per chain
+    for d <= 16, two lanes per chain for 16 < d <= 32 (RAM: lane per chain), wave per chain beyond; regression
+    kernels have their own fixed order (the oracle picks it from the model)."""
+    return None
 
 
 def fixture_path(name):

@@ -113,17 +113,35 @@ def oracle_sampler(sp) -> OSampler:
     return o
 
 
-class OracleChains:
-    """The oracle's twin of an MCMCTask: per-chain state kept between runs."""
+ORDER_PAIR = -2          # oracle.c ORC_ORDER_PAIR: two lanes per chain (16 < d <= 32)
 
-    def __init__(self, m, sampler, nchains, seed=1, chain_offset=0, init_x=None, order=0):
+
+def kernel_order(m, sampler_kind=None):
+    """The summation order of the kernel family the library runs for this model / sampler:
+    regression targets have their own fixed order (the oracle picks it from the model: 0 here); RAM (kind 5) runs
+    lane per chain up to d = 32 (order 0) and wave per chain beyond (1); every other separable case: lane per
+    chain for d <= 16 (0), two lanes per chain for 16 < d <= 32 (ORDER_PAIR), wave per chain up to 2048 (1),
+    block per chain of 4 / 8 waves up to 8192 / 16384."""
+    d = m.size
+    if getattr(m.target, "X", None) is not None:         # logistic / linear regression
+        return 0
+    if sampler_kind == 5:
+        return 0 if d <= 32 else 1
+    return 0 if d <= 16 else ORDER_PAIR if d <= 32 else 1 if d <= 2048 else 4 if d <= 8192 else 8
+
+
+class OracleChains:
+    """The oracle's twin of an MCMCTask: per-chain state kept between runs.  order None: the library's own
+    (kernel_order)."""
+
+    def __init__(self, m, sampler, nchains, seed=1, chain_offset=0, init_x=None, order=None):
         self.om = OracleModel(m)
         self.os = oracle_sampler(sampler)
         self.kind = sampler.kind
         self.C = int(nchains)
         self.seed = int(seed)
         self.chain0 = int(chain_offset)
-        self.order = int(order)
+        self.order = int(kernel_order(m, sampler.kind) if order is None else order)
         d, C = m.size, self.C
         if init_x is None:
             self.x = np.ascontiguousarray(np.repeat(self.om.init[:, None], C, axis=1))
@@ -185,13 +203,15 @@ class OracleChains:
         return samples, grads, acc
 
 
-def seqmc(targets, particles, steps, burnin, trigger, seed, target_seeds, order=0):
+def seqmc(targets, particles, steps, burnin, trigger, seed, target_seeds, order=None):
     """orc_seqmc: run_seqmc (SeqMC.jl:43-122) over [(model, sampler), ...] with particles [npart, d].
     Returns samples [steps-burnin][d][npart], weights [steps-burnin][npart], resampled flags [steps][nt]."""
     P = np.asarray(particles, dtype=np.float64)
     npart, d = P.shape
     chains = [OracleChains(m, s, nchains=npart, seed=ts, order=order) for (m, s), ts in zip(targets, target_seeds)]
     nt = len(chains)
+    if order is None:
+        order = chains[0].order
     models = (ct.POINTER(OModel) * nt)(*[ct.pointer(c.om.s) for c in chains])
     samplers = (ct.POINTER(OSampler) * nt)(*[ct.pointer(c.os) for c in chains])
     states = (ct.POINTER(OState) * nt)(*[ct.pointer(c.st) for c in chains])
@@ -213,7 +233,10 @@ def seqmc(targets, particles, steps, burnin, trigger, seed, target_seeds, order=
     return samples, weights, flags
 
 
-def eval_batch(m, xs, order=0):
+def eval_batch(m, xs, order=None):
+    """model.eval / evalallg of every column; order None: the library's eval kernel's order (kernel_order)"""
+    if order is None:
+        order = kernel_order(m)
     om = OracleModel(m)
     xs = np.ascontiguousarray(np.asarray(xs, dtype=np.float64).reshape(m.size, -1))
     C = xs.shape[1]

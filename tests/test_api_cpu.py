@@ -193,14 +193,23 @@ def test_bench_traffic_only_from_a_profile_of_the_same_kernel():
 
 
 def test_bench_valu_roofline_profile():
-    """The metric kernel's VALU roofline inputs come from a committed PMC profile of that kernel instance, and
-    the implied fraction of VALU issue peak is a fraction (<= 1)"""
+    """A VALU profile prices a run only when it was recorded from the same step-kernel sources, for the same kernel
+    instance and the same workload (steps included); every committed profile implies a VALU fraction <= 1 at its
+    own measured clock."""
     import importlib
+    import json
     bench = importlib.import_module("bench")
-    vm = bench.measured_valu("lpc_rwm<8, true, IsoDot, true>")
-    assert vm is not None and os.path.exists(os.path.join(ROOT, vm["source"]))
-    assert 0.0 < vm["valu_busy"] <= 1.0
-    # at the profiled dispatch: cycles per chain-step x chain-steps / duration against 1024 SIMDs x 2.4 GHz
-    units = 1048576 * (20 if "steps=20" in vm["workload_key"] else 1000)
-    frac = 4 * vm["valu_quadcycles_per_chain_step"] * units / vm["duration_s"] / (bench.VALU_PEAK_TCYC * 1e12)
-    assert 0.3 < frac <= 1.0
+    prof = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
+    h = bench.step_kernel_src_hash()
+    for k, e in prof.items():
+        got = bench.measured_valu(e["kernel"], e["workload_key"])
+        assert (got is not None) == (e["src_hash"] == h)
+        assert bench.measured_valu(e["kernel"], e["workload_key"] + "x") is None      # another workload
+        assert bench.measured_valu("lpc_rwm<9,true,X,true>", e["workload_key"]) is None
+        assert os.path.exists(os.path.join(ROOT, e["source"]))
+        assert 0.0 < e["valu_busy"] <= 1.0
+        steps = int(e["workload_key"].split("steps=")[1].split("|")[0])
+        chains = int(e["workload_key"].split("chains=")[1].split("|")[0])
+        cyc = 4 * e["valu_quadcycles_per_chain_step"] * chains * steps       # VALU issue cycles of the launch
+        frac_at_clock = cyc / e["duration_s"] / (1024 * e["clock_ghz"] * 1e9)
+        assert 0.3 < frac_at_clock <= 1.0 + 1e-6, (k, frac_at_clock)

@@ -6,7 +6,8 @@ same, so the runtime launches the uniform-scale specialisations (`scale1` in a s
 run those workloads' own configurations, read back which step kernel ran (`mcmc_chains_step_kernel`), and
 compare the HIP results with the oracle bit for bit:
 
-- config 2 (d=3) -> `lpc_rwm<1, false, IsoDot, true>`; the metric (d=32) -> `lpc_rwm<8, true, IsoDot, true>`;
+- config 2 (d=3) -> `lpc_rwm<1, false, IsoDot, true>`; the metric (d=32) -> `lpp_rwm<4, true, IsoDot, true>` (two
+  lanes per chain, samplers.hpp PairChain);
 - config 1 (one chain, d <= 4) -> the path-speculation kernel `lpc_rwm_spec`; C <= 64 -> the
   look-ahead kernel `lpc_rwm_la`; both also across launches
   (`steps_per_launch`) and continued runs, where a launch starts mid-way through the kept range;
@@ -35,10 +36,14 @@ def _check(chain, s_ref, acc_ref):
 
 @pytest.mark.parametrize("d,C,kernel", [
     (3, 1000, "lpc_rwm<1, false, IsoDot, true>"),      # config 2's instance
-    (32, 1000, "lpc_rwm<8, true, IsoDot, true>"),      # the metric's instance
+    (32, 1000, "lpp_rwm<4, true, IsoDot, true>"),      # the metric's instance
     (4, 300, "lpc_rwm<1, true, IsoDot, true>"),
-    (17, 130, "lpc_rwm<5, false, IsoDot, true>"),
-    (32, 65, "lpc_rwm<8, true, IsoDot, true>"),        # one chain past the look-ahead limit
+    (16, 300, "lpc_rwm<4, true, IsoDot, true>"),       # the last lane-per-chain width
+    (17, 130, "lpp_rwm<3, false, IsoDot, true>"),
+    (24, 130, "lpp_rwm<3, true, IsoDot, true>"),
+    (30, 97, "lpp_rwm<4, false, IsoDot, true>"),
+    (32, 65, "lpp_rwm<4, true, IsoDot, true>"),        # one chain past the look-ahead limit
+    (32, 64, "lpc_rwm_la<8, IsoDot, true>"),           # the look-ahead kernel in the pair kernels' sum order
 ])
 def test_uniform_scale_rwm_instances(gpu, d, C, kernel):
     m = _readme_model(d)
@@ -56,7 +61,7 @@ def test_nonuniform_scale_takes_the_generic_instance(gpu):
     m = mc.model(mc.IsoNormalDot(), init=np.ones(32), scale=np.linspace(0.8, 1.2, 32))
     t = (m * mc.RWM(0.1) * mc.SerialMC(steps=10)).batch(128, seed=1)
     mc.run(t)
-    assert t.step_kernel == "lpc_rwm<8, true, IsoDot, false>"
+    assert t.step_kernel == "lpp_rwm<4, true, IsoDot, false>"
 
 
 @pytest.mark.parametrize("uniform", [True, False])
@@ -124,7 +129,7 @@ def test_full_size_metric_run(gpu):
     cfg = r.cfg()
     _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
     torch.cuda.synchronize(dev)
-    assert t.step_kernel == "lpc_rwm<8, true, IsoDot, true>"
+    assert t.step_kernel == "lpp_rwm<4, true, IsoDot, true>"
     assert out.nkept == 90
 
     starts = np.unique(np.linspace(0, C - 64, 64).astype(np.int64) // 64 * 64)

@@ -150,9 +150,11 @@ def assert_parity(chain, s_ref, g_ref, acc_ref, kind):
 
 
 def order_for(d):
-    """lane-per-chain kernels (d <= 32) sum left to right; wave-per-chain kernels (d <= 2048) per lane + butterfly;
-    block-per-chain kernels (d <= 8192: 4 waves, d <= 16384: 8 waves) per lane, per wave, then waves left to right."""
-    return 0 if d <= 32 else 1 if d <= 2048 else 4 if d <= 8192 else 8
+    """None: the oracle takes the library's own order (oracle_ref.kernel_order): lane-per-chain kernels (d <= 16)
+    sum left to right; two-lanes-per-chain kernels (16 < d <= 32) each half, then the halves; wave-per-chain kernels
+    (d <= 2048) per lane + butterfly; block-per-chain kernels (d <= 8192: 4 waves, d <= 16384: 8 waves) per lane,
+    per wave, then waves left to right; RAM lane per chain up to d = 32."""
+    return None
 
 
 @pytest.mark.parametrize("sname", list(SAMPLERS))

@@ -74,7 +74,19 @@ CASES = {
     "logistic_mala": lambda: (_logistic(), mc.MALA(0.01), mc.SerialMC(steps=10, burnin=2, thinning=3), 257),
     "hmcda_dist": lambda: (mc.model(mc.DistDSL("Gamma", 3, 0.2), x=0.6, gradient=True), mc.HMCDA(),
                            mc.SerialMC(steps=40, burnin=20), 130),
+    # RAM (RAM.jl:41-79): per-block jump factors, assembled by MCMCTask.ram_factor from every block's
+    # mcmc_chains_ram_factor -- wave per chain (d = 70) and the regression layout (d = 10)
+    "ram70": lambda: (mc.model(mc.IsoNormalDot(), init=np.ones(70), grad=True), mc.RAM(1.0, 0.234),
+                      mc.SerialMC(steps=30, burnin=5, thinning=5), 150),
+    "ram_linear10": lambda: (_linear10(), mc.RAM(1.0, 0.3), mc.SerialMC(steps=25, burnin=5, thinning=4), 200),
 }
+
+
+def _linear10(n=60):
+    rng = np.random.default_rng(6)
+    X = np.hstack([np.ones((n, 1)), rng.normal(size=(n, 9))])
+    Y = X @ rng.normal(size=10) + rng.normal(size=n)
+    return mc.model(mc.LinearRegression(X, Y), vars=np.zeros(10), gradient=True)
 
 
 @pytest.mark.gpu
@@ -89,6 +101,8 @@ def test_group_equals_one_context(gpu, case, devices):
     assert grp.diagnostics["gather_s"] >= 0.0
     assert task.evals == one.task.evals
     assert task.steps_done == one.task.steps_done == r.len
+    if isinstance(s, mc.RAM):
+        assert np.array_equal(task.ram_factor().view(np.uint64), one.task.ram_factor().view(np.uint64))
     # continue (run(chain), runners.jl:14) and resume (SerialMC.jl:93-97) on the group
     _same(mc.run(grp), mc.run(one))
     _same(mc.resume(grp, steps=7), mc.resume(one, steps=7))
@@ -182,3 +196,57 @@ def test_two_host_threads_two_contexts_one_gpu(gpu):
         assert np.array_equal(res[i][0].view(np.uint64), alone[i]._samples.view(np.uint64))
         bits = np.unpackbits(res[i][1].view(np.uint8).reshape(len(r.r), -1), axis=1, bitorder="little")
         assert np.array_equal(bits.astype(bool).T, alone[i].diagnostics["accept"])
+
+
+@pytest.mark.gpu
+def test_group_failed_block_blocks_further_runs(gpu):
+    """A run in which one block fails leaves the blocks at different steps: the error names the block, and the
+    chains refuse further runs (and steps_done) until reset; after mcmc_group_chains_reset (resume) the group is
+    again bit-identical to one context."""
+    lib = _lib.load()
+    m, s, r, C = CASES["hmc3"]()
+    task = (m * s * r).batch(C, seed=11, devices=(0, 0, 0))
+    mc.run(task)
+    _lib.check(lib.mcmc_debug_group_inject_failure(task.handle(), 1))
+    with pytest.raises(_lib.MCMCError, match="block 1"):
+        mc.run(task)
+    with pytest.raises(_lib.MCMCError, match="different steps"):
+        task.steps_done
+    with pytest.raises(_lib.MCMCError, match="failed"):
+        mc.run(task)
+    task.reset()
+    assert task.steps_done == 0
+    _same(mc.run(task), mc.run((m * s * r).batch(C, seed=11)))
+
+
+@pytest.mark.gpu
+def test_group_gather_rate_at_metric_size(gpu):
+    """The end gather at 2^20 chains (d = 32, 20 kept rows: 5.4 GB of samples into one host buffer), two blocks:
+    the caller's pageable buffers are page-locked for the run (hipHostRegister), so each block's strided copy
+    is direct DMA.  Prints the measured gather time and rate; DESIGN.md §8 quotes it."""
+    import json
+    import time
+    C, d = 1 << 20, 32
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(d))
+    r = mc.SerialMC(steps=20, burnin=0, thinning=1)
+    task = (m * mc.RWM(0.1) * r).batch(C, seed=1, devices=(0, 0))
+    h = task.handle()
+    lib = _lib.load()
+    nk = len(r.r)
+    samples = np.empty((nk, d, C))
+    bits = np.empty((nk, C // 64), dtype=np.uint64)
+    samples[:, :, ::4096] = 0.0                                  # touch nothing else: registration faults pages in
+    out = _lib.Outputs()
+    out.samples, out.accept_bits = samples.ctypes.data, bits.ctypes.data
+    cfg = r.cfg()
+    gs = ct.c_double(0.0)
+    t0 = time.perf_counter()
+    _lib.check(lib.mcmc_group_run_serialmc(h, ct.byref(cfg), ct.byref(out), ct.byref(gs)))
+    wall = time.perf_counter() - t0
+    nbytes = samples.nbytes + bits.nbytes
+    line = {"test": "group_gather", "chains": C, "d": d, "kept": nk, "blocks": 2, "bytes": nbytes,
+            "gather_s": gs.value, "gather_GBps": nbytes / gs.value / 1e9, "step_loop_s": out.runtime_s,
+            "call_wall_s": wall}
+    print(json.dumps(line))
+    assert np.isfinite(samples[-1]).all() and samples[-1, :, ::65536].std() > 0
+    assert nbytes / gs.value > 5e9, line                         # direct DMA, not staged pageable copies

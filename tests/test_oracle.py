@@ -302,6 +302,39 @@ def test_wave_order_reduction_is_a_sum():
     assert np.allclose(lp0, lp1, rtol=1e-13) and np.array_equal(g0, g1)
 
 
+def _fma(a, b, c):
+    """correctly rounded a*b + c (Python 3.10 has no math.fma): exact rational arithmetic, one rounding"""
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+@pytest.mark.parametrize("d", [17, 20, 24, 29, 32])
+def test_pair_order_is_the_two_halves(d):
+    """ORDER_PAIR (two lanes per chain, 16 < d <= 32): the first 4 ceil(ceil(d/4)/2) coordinates left to right, the
+    rest left to right, then the two partial sums -- restated here in that exact order, bitwise (fma chains as the
+    kernels form them); it is also the default order at these widths (oracle_ref.kernel_order), and RAM stays
+    lane per chain."""
+    x = np.random.default_rng(d).normal(size=(d, 5))
+    S = 4 * ((((d + 3) // 4) + 1) // 2)
+    m_iso = mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
+    lp, _ = orc.eval_batch(m_iso, x, order=orc.ORDER_PAIR)
+    lp0, _ = orc.eval_batch(m_iso, x, order=0)
+    for c in range(5):
+        a = b = 0.0
+        for j in range(d):
+            if j < S:
+                a = _fma(x[j, c], x[j, c], a)
+            else:
+                b = _fma(x[j, c], x[j, c], b)
+        assert lp[c] == -(a + b)
+        seq = 0.0
+        for j in range(d):
+            seq = _fma(x[j, c], x[j, c], seq)
+        assert lp0[c] == -seq
+    assert orc.kernel_order(m_iso, 1) == orc.ORDER_PAIR and orc.kernel_order(m_iso, 5) == 0
+    assert np.array_equal(orc.eval_batch(m_iso, x)[0], lp)           # the default is the library's order
+
+
 def test_init_out_of_support_raises():
     m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.zeros(2), gradient=True)
     with pytest.raises(AssertionError, match="out of model support"):
