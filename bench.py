@@ -317,7 +317,7 @@ def main():
     # MCMC_BENCH_BACKEND=gloo: rehearse the multi-rank path on a 1-GPU box (ranks share cuda:0, host-side
     # reductions); the driver's N-GPU runs use the default, RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("MCMC_BENCH_BACKEND", "nccl")
-    if world > 1:
+    if world > 1 or "MASTER_ADDR" in os.environ:        # under torchrun: the process group even for N = 1
         import torch.distributed as dist
         if backend == "gloo":
             local = local % max(1, torch.cuda.device_count())
@@ -587,6 +587,7 @@ def main():
             "burnin": burnin, "thinning": args.thinning, "kept_per_chain": nkept,
             "steps_per_launch": spl, "evals": evals, "key": wkey,
             "parallelism": f"chains sharded over {world} GPU(s), no collective in the step loop",
+            "process_group": (("nccl (RCCL)" if backend == "nccl" else backend) if dist is not None else None),
         },
         "roofline": roof,
         "acceptance": acceptance,

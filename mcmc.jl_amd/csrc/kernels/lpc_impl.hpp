@@ -489,7 +489,8 @@ static hipError_t lpc_record_m(const KernelArgs& a, const LeapRec& r, hipStream_
 // defines mcmc_lpc_ram_iso.
 namespace mcmc {
 template <int NB, class M>
-__global__ __launch_bounds__(kBlock, NB <= 4 ? 2 : 1) void lpc_ram(KernelArgs a) { ram_body<LaneChain<NB, false>, M>(a); }
+// d > 16: the log-target in PairChain's order (LaneChain SPLIT), as the chains' model.eval (lpp_eval) forms it
+__global__ __launch_bounds__(kBlock, NB <= 4 ? 2 : 1) void lpc_ram(KernelArgs a) { ram_body<LaneChain<NB, false, (NB > 4)>, M>(a); }
 
 template <class M>
 static hipError_t lpc_ram_step(const KernelArgs& a, hipStream_t st) {

@@ -89,31 +89,65 @@ end
 
 # ---- prun (runners.jl:35-42, examples/parallel_serialmc.jl) -> one chain batch over a node's GPUs
 # mcmc_group_*: contiguous 64-chain-aligned blocks, one per listed device, driven from this one Julia thread
-# (a library worker thread per block); results bit-identical to one context running every chain.
-function group(devices::Vector{Int32} = Int32.(0:7))
+# (a library worker thread per block); results bit-identical to one context running every chain.  Blocks are whole
+# 64-chain groups, so a batch of fewer than 64 N chains leaves trailing devices idle.  The handles are freed by
+# finalizers (or destroy! explicitly); a GroupChains keeps its Group alive, so the group is destroyed after them.
+mutable struct Group
+    h::Ptr{Cvoid}
+    function Group(h)
+        g = new(h)
+        finalizer(destroy!, g)
+    end
+end
+mutable struct GroupChains
+    h::Ptr{Cvoid}
+    group::Group
+    function GroupChains(h, g)
+        gc = new(h, g)
+        finalizer(destroy!, gc)
+    end
+end
+function destroy!(gc::GroupChains)
+    gc.h == C_NULL || ccall((:mcmc_group_chains_destroy, lib), Cint, (Ptr{Cvoid},), gc.h)
+    gc.h = C_NULL
+end
+function destroy!(g::Group)
+    g.h == C_NULL || ccall((:mcmc_group_destroy, lib), Cint, (Ptr{Cvoid},), g.h)
+    g.h = C_NULL
+end
+
+function device_count()
+    n = Ref{Cint}(0)
+    check(ccall((:mcmc_device_count, lib), Cint, (Ptr{Cint},), n))
+    Int(n[])
+end
+
+# default: every visible device
+function group(devices::Vector{Int32} = Int32.(0:device_count()-1))
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:mcmc_group_create, lib), Cint, (Ptr{Int32}, Int32, Ptr{Ptr{Cvoid}}), devices, length(devices), h))
-    h[]
+    Group(h[])
 end
 
 # the model descriptor is uploaded once per device; init/scale (and X/Y) must stay rooted during the call
-function group_chains(g, desc::ModelDesc, s::SamplerCfg, nchains; seed = 1, offset = 0, roots = ())
+function group_chains(g::Group, desc::ModelDesc, s::SamplerCfg, nchains; seed = 1, offset = 0, roots = ())
     h = Ref{Ptr{Cvoid}}(C_NULL)
     GC.@preserve roots check(ccall((:mcmc_group_chains_create, lib), Cint,
         (Ptr{Cvoid}, Ref{ModelDesc}, Ref{SamplerCfg}, Int64, Int64, UInt64, Ptr{Float64}, Ptr{Ptr{Cvoid}}),
-        g, desc, s, nchains, offset, seed, C_NULL, h))
-    h[]
+        g.h, desc, s, nchains, offset, seed, C_NULL, h))
+    GroupChains(h[], g)
 end
 
 # every block's step loop concurrently, then each GPU's outputs device -> host into its columns of smp / bits
-function run_serialmc_group(gc, d, C; steps, burnin = 0, thinning = 1)
+# (the library page-locks smp / bits for the call, so the gather is direct DMA)
+function run_serialmc_group(gc::GroupChains, d, C; steps, burnin = 0, thinning = 1)
     r = (burnin+1):thinning:steps
     smp = Array{Float64}(undef, C, d, length(r))
     bits = zeros(UInt64, cld(C, 64), length(r))
     out = Outputs(pointer(smp), C_NULL, pointer(bits), C_NULL, C_NULL, 0, 0.0, 0.0, 0)
     gather = Ref{Float64}(0.0)
     GC.@preserve smp bits check(ccall((:mcmc_group_run_serialmc, lib), Cint,
-        (Ptr{Cvoid}, Ref{RunnerCfg}, Ref{Outputs}, Ref{Float64}), gc, RunnerCfg(burnin, thinning, steps), out, gather))
+        (Ptr{Cvoid}, Ref{RunnerCfg}, Ref{Outputs}, Ref{Float64}), gc.h, RunnerCfg(burnin, thinning, steps), out, gather))
     accept = [(bits[fld(c, 64) + 1, j] >> (c % 64)) & 1 == 1 for c in 0:C-1, j in 1:length(r)]
     smp, accept, out.runtime_s, gather[]
 end

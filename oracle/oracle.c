@@ -569,7 +569,7 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
             double* Lc = st->ram_L + c;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* rvec = randn(d) */
             double nz = 0.0;                                                  /* dot(rvec, rvec): in order, */
-            if (order == 0 || orc_is_glm(m))                                  /* or in the wave order of the */
+            if (order == 0 || order == ORC_ORDER_PAIR || orc_is_glm(m))       /* or in the wave order of the */
                 for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);     /* wave-per-chain kernel (d > 32) */
             else
                 nz = orc_dot(mom, m, order);

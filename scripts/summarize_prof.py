@@ -20,7 +20,7 @@ src, tag = sys.argv[1], sys.argv[2]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
-STEP_KERNELS = ("mcmc::lpc_", "mcmc::wpc_", "mcmc::glm_rwm", "mcmc::glm_mala", "mcmc::glm_hmc", "mcmc::glm_ram")
+STEP_KERNELS = ("mcmc::lpc_", "mcmc::lpp_", "mcmc::wpc_", "mcmc::glm_rwm", "mcmc::glm_mala", "mcmc::glm_hmc", "mcmc::glm_ram")
 
 
 def rows(kind, name):

@@ -118,15 +118,13 @@ ORDER_PAIR = -2          # oracle.c ORC_ORDER_PAIR: two lanes per chain (16 < d 
 
 def kernel_order(m, sampler_kind=None):
     """The summation order of the kernel family the library runs for this model / sampler:
-    regression targets have their own fixed order (the oracle picks it from the model: 0 here); RAM (kind 5) runs
-    lane per chain up to d = 32 (order 0) and wave per chain beyond (1); every other separable case: lane per
-    chain for d <= 16 (0), two lanes per chain for 16 < d <= 32 (ORDER_PAIR), wave per chain up to 2048 (1),
-    block per chain of 4 / 8 waves up to 8192 / 16384."""
+    regression targets have their own fixed order (the oracle picks it from the model: 0 here); separable targets:
+    lane per chain for d <= 16 (0), two lanes per chain for 16 < d <= 32 (ORDER_PAIR; RAM runs lane per chain there
+    but sums its log-target in that order, its |z|^2 left to right), wave per chain up to 2048 (1), block per chain
+    of 4 / 8 waves up to 8192 / 16384."""
     d = m.size
     if getattr(m.target, "X", None) is not None:         # logistic / linear regression
         return 0
-    if sampler_kind == 5:
-        return 0 if d <= 32 else 1
     return 0 if d <= 16 else ORDER_PAIR if d <= 32 else 1 if d <= 2048 else 4 if d <= 8192 else 8
 
 

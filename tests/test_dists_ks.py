@@ -170,3 +170,28 @@ def test_readme_hmc_statistics_hip(gpu):
     x = ch._samples[::10].reshape(-1)
     assert abs(x.std() - math.sqrt(0.5)) < 0.01
     assert ks_value(x[::7], stats.norm(0, math.sqrt(0.5))) < KS_CRIT_001
+    # README.md:178-204: var(mychain2) under vtype :imse, :iid, :ipse and :bm (variance of the chain mean; var.jl
+    # 7-8, 45-118), one README chain per parameter.  On the device for every chain (kernels/stats.hip); the iid
+    # variance from ESS = n var_iid / var_imse (ess.jl:6-10).  Each README value must be a plausible single-chain
+    # draw -- inside the 0.5-99.5 % range of the 1 024 chains' estimates -- and the chains' median must sit within
+    # the sampling spread of one chain (per-chain relative sd: ~2 % iid, ~4 % IMSE/IPSE, ~15 % batch means).
+    readme = {"imse": [9.26753e-5, 9.28578e-5, 9.17639e-5], "iid": [5.49207e-5, 5.50308e-5, 5.43862e-5],
+              "ipse": [9.26753e-5, 9.28578e-5, 9.17639e-5], "bm": [9.13673e-5, 9.40208e-5, 7.33864e-5]}
+    n = ch._samples.shape[0]
+    est = {}
+    for vt in ("imse", "ipse", "bm"):
+        e_vt, v_vt = mc.stats.ess_device(ch, vt, return_var=True)           # [C][d] each
+        est[vt] = v_vt
+        if vt == "imse":
+            est["iid"] = e_vt * v_vt / n
+    rel = {"iid": 0.06, "imse": 0.12, "ipse": 0.12, "bm": 0.45}
+    for vt, ref in readme.items():
+        v = est[vt]
+        for j in range(3):
+            lo, hi = np.quantile(v[:, j], [0.005, 0.995])
+            assert lo <= ref[j] <= hi, (vt, j, ref[j], lo, hi)
+            assert abs(np.median(v[:, j]) / ref[j] - 1) < rel[vt], (vt, j, np.median(v[:, j]), ref[j])
+    # the host restatement of var.jl (stats.py) agrees with the device's iid and batch-means estimators
+    for vt in ("iid", "bm"):
+        host = mc.stats.var(ch, vt)                                           # [C][d] (numpy, var.jl)
+        assert np.allclose(host, est[vt], rtol=1e-9), vt

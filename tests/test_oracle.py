@@ -312,8 +312,7 @@ def _fma(a, b, c):
 def test_pair_order_is_the_two_halves(d):
     """ORDER_PAIR (two lanes per chain, 16 < d <= 32): the first 4 ceil(ceil(d/4)/2) coordinates left to right, the
     rest left to right, then the two partial sums -- restated here in that exact order, bitwise (fma chains as the
-    kernels form them); it is also the default order at these widths (oracle_ref.kernel_order), and RAM stays
-    lane per chain."""
+    kernels form them); it is also the default order at these widths (oracle_ref.kernel_order), RAM included."""
     x = np.random.default_rng(d).normal(size=(d, 5))
     S = 4 * ((((d + 3) // 4) + 1) // 2)
     m_iso = mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
@@ -331,7 +330,7 @@ def test_pair_order_is_the_two_halves(d):
         for j in range(d):
             seq = _fma(x[j, c], x[j, c], seq)
         assert lp0[c] == -seq
-    assert orc.kernel_order(m_iso, 1) == orc.ORDER_PAIR and orc.kernel_order(m_iso, 5) == 0
+    assert orc.kernel_order(m_iso, 1) == orc.ORDER_PAIR == orc.kernel_order(m_iso, 5)
     assert np.array_equal(orc.eval_batch(m_iso, x)[0], lp)           # the default is the library's order
 
 
