@@ -310,6 +310,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one process per GPU is required")
+    # the contract is ONE JSON line on stdout: libraries that print to fd 1 (RCCL's version banner at
+    # init_process_group, gloo's connection lines) are sent to stderr; the line goes to the saved stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -603,7 +608,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,
                                             C=min(C, 4096 if cfg0["model"] == "iso" else 64))
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()                                  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()

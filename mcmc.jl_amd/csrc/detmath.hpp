@@ -249,6 +249,37 @@ __device__ __forceinline__ double bm_log_u32(uint32_t w, const double (*tab)[4] 
     return hi + lo;
 }
 
+// The Box-Muller radius^2, -2 log((w + 0.5) 2^-32): bm_log_u32 with every operation scaled by -2 -- the table rows
+// (kBmRad512Tab = -2 x kBmLog512Tab's), the reduced argument r2 = fma(m, -2 inv_c, 2) = -2 r, the log1p stages
+// (each an exact power-of-two multiple of bm_log_u32's) and the e ln2 terms -- so the result is bitwise
+// -2.0 * bm_log_u32(w) (the oracle's -2.0 * orc_bm_log_u32) without the final multiply.  Round 3.
+static __device__ const double kBmRad512Tab[512][4] = {BM_RAD512_TABLE_ROWS};
+
+__device__ __forceinline__ double bm_rad2_u32(uint32_t w, const double (*tab)[4] = kBmRad512Tab) {
+    const double m2ln2_hi = -0x1.62e42fee00000p+0;                      // -2 ln2_hi, -2 ln2_lo
+    const double m2ln2_lo = -0x1.a39ef35793c76p-32;
+    const double x = (double)w + 0.5;
+    const uint64_t b = d2bits(x);
+    const uint32_t xh = (uint32_t)(b >> 32);
+    const uint32_t up = (xh >> 19) & 1u;
+    const int e = (int)(xh >> 20) + (int)up - (1023 + 32);
+    const uint32_t mhi = ((0x3ffu ^ up) << 20) | (xh & 0x000fffffu);
+    const double m = bits2d(((uint64_t)mhi << 32) | (b & 0xffffffffull));
+    typedef double f64x2_t __attribute__((ext_vector_type(2)));
+    const f64x2_t* row = reinterpret_cast<const f64x2_t*>(reinterpret_cast<const char*>(tab) + ((xh >> 6) & 0x3fe0u));
+    const f64x2_t a = row[0], t = row[1];                               // (-2 inv_c, -2 T_hi), (-2 T_lo, 0)
+    const double r2 = __builtin_fma(m, a.x, 2.0);                       // -2 r
+    double Q = __builtin_fma(r2, 0x1.5555555555555p-8, 0x1.999999999999ap-7);   // P stages x 1/16, -1/8, 1/4, -1/2
+    Q = __builtin_fma(r2, Q, 0x1p-5);
+    Q = __builtin_fma(r2, Q, 0x1.5555555555555p-4);
+    Q = __builtin_fma(r2, Q, 0x1p-2);
+    const double p2 = __builtin_fma(r2 * r2, Q, r2);                   // -2 log1p(r)
+    const double de = (double)e;
+    const double hi = __builtin_fma(de, m2ln2_hi, a.y);
+    const double lo = __builtin_fma(de, m2ln2_lo, t.x) + p2;
+    return hi + lo;
+}
+
 typedef double dm_f64x2 __attribute__((ext_vector_type(2)));
 
 // exp for the logistic likelihood (prob = 1/(1+exp(-X*vars)), examples/logistic_regression.jl:19), table-
@@ -409,18 +440,18 @@ __device__ __forceinline__ double sqrt_pos_normal(double x) {
 
 // Two Box-Muller pairs from one Philox block: radius sqrt(-2 log u1), u1 = (w.x + 1/2) 2^-32 in (0,1);
 // angle 2 pi u2, u2 = w.y 2^-32.
-// tab, sct: the radius-log and angle tables, in global memory (default) or a kernel's LDS copies
+// tab, sct: the radius^2 (bm_rad2_u32) and angle tables, in global memory (default) or a kernel's LDS copies
 __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3,
-                                         const double (*tab)[4] = kBmLog512Tab,
+                                         const double (*tab)[4] = kBmRad512Tab,
                                          const double (*sct)[2] = kBmSinCos1024Tab) {
     {
-        const double rad = sqrt_pos_normal(-2.0 * bm_log_u32(w.x, tab));
+        const double rad = sqrt_pos_normal(bm_rad2_u32(w.x, tab));
         double s, c;
         det_sincos2pi_u32(w.y, s, c, sct);
         z0 = rad * c; z1 = rad * s;
     }
     {
-        const double rad = sqrt_pos_normal(-2.0 * bm_log_u32(w.z, tab));
+        const double rad = sqrt_pos_normal(bm_rad2_u32(w.z, tab));
         double s, c;
         det_sincos2pi_u32(w.w, s, c, sct);
         z2 = rad * c; z3 = rad * s;

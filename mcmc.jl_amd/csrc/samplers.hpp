@@ -40,7 +40,7 @@ template <int NT = kBlock>
 __device__ __forceinline__ void stage_bm_tables(double (*lt)[4], double (*ls)[2]) {
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
     constexpr int kN = 1024 / NT;                           // 16-byte rows per thread per table
-    const f64x2_t* gt = reinterpret_cast<const f64x2_t*>(&kBmLog512Tab[0][0]);
+    const f64x2_t* gt = reinterpret_cast<const f64x2_t*>(&kBmRad512Tab[0][0]);
     const f64x2_t* gs = reinterpret_cast<const f64x2_t*>(&kBmSinCos1024Tab[0][0]);
     f64x2_t a[kN], b[kN];
 #pragma unroll
@@ -76,6 +76,7 @@ struct LaneChain {
     static constexpr int NC = 4 * NB_;
     static constexpr int kSplit = SPLIT ? 4 * ((NB_ + 1) / 2) : 0;
     static constexpr int kChainsPerBlock = kBlock;
+    static constexpr bool kPairs = false;
     int64_t c;        // local chain index
     bool live;        // c < C
     int d;
@@ -173,6 +174,7 @@ struct PairChain {
     static constexpr int NB = NB_;
     static constexpr int NC = 4 * NB_;
     static constexpr int kChainsPerBlock = kBlock / 2;
+    static constexpr bool kPairs = true;
     int64_t c;        // local chain index
     bool live;
     int d;
@@ -192,6 +194,15 @@ struct PairChain {
     __device__ __forceinline__ int coord(int k) const { return h * NC + k; }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(h * NB + b); }
+    // half `which`'s value of v in both lanes of the chain (v_permlane32_swap: {half 0's, half 1's} broadcasts)
+    __device__ __forceinline__ double from_half(double v, int which) const {
+        const uint64_t u = (uint64_t)__double_as_longlong(v);
+        const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        return which == 0 ? __longlong_as_double((long long)(((uint64_t)b[0] << 32) | a[0]))
+                          : __longlong_as_double((long long)(((uint64_t)b[1] << 32) | a[1]));
+    }
     // (half 0's value) + (half 1's value) in both lanes of the chain, bitwise the same
     __device__ __forceinline__ double reduce(double v) const {
         const uint64_t u = (uint64_t)__double_as_longlong(v);
@@ -298,6 +309,7 @@ template <int G, bool FULL = false, int W = 1>
 struct WaveChain {
     static constexpr int NB = G;
     static constexpr int NC = 4 * G;
+    static constexpr bool kPairs = false;
     static constexpr int L = 64 * W;                    // lanes per chain
     int64_t c;
     bool live;
@@ -442,6 +454,33 @@ __device__ __forceinline__ bool mh_accept_short_circuit(const Stream& rs, uint32
     return acc;
 }
 
+// The RWM / MALA test of step i (launch step t), RWM.jl:63 / MALA.jl:108.  PairChain: both lanes of a chain need
+// the same uniform, so on even t the two halves draw steps i (half 0) and i + 1 (half 1) from the counter-based
+// stream at once; half 0's draw is broadcast now and half 1's kept for step t + 1 -- one Philox block per chain per
+// two steps, the same values as mh_accept_short_circuit's conditional draw (the stream is keyed by (chain, step)).
+template <class P>
+struct AcceptDraw {
+    double u_next = 0.0;
+    __device__ __forceinline__ bool test(const P& p, const Stream& rs, uint32_t chain, int64_t i, int t, double ratio) {
+        if constexpr (P::kPairs) {
+            double u;
+            if ((t & 1) == 0) {
+                const u32x4 w = rs.block(chain, (uint32_t)(i + p.h), 0u, TAG_ACCEPT);
+                const double uu = uniform53(w.x, w.y);
+                u = p.from_half(uu, 0);
+                u_next = uu;
+            } else {
+                u = p.from_half(u_next, 1);
+            }
+            bool acc = ratio > 0.0;
+            if (!acc) acc = gt_det_log(ratio, u);
+            return acc;
+        } else {
+            return mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        }
+    }
+};
+
 // tuner adaptation factor (MALA.jl:36-39, HMC.jl:165-169)
 __device__ __forceinline__ double tune_factor(int32_t acc, int32_t prop, double target) {
     const double rate = (double)acc / (double)prop;
@@ -463,6 +502,7 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     p.stage();
 #pragma unroll
     for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
+    AcceptDraw<P> ad;
 
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
@@ -473,7 +513,7 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
         bool oos;
         const double lpp = eval_lp(p, model, xp, oos);
         const double ratio = lpp - lp;
-        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        const bool acc = ad.test(p, rs, chain, i, t, ratio);
         if (acc) {
 #pragma unroll
             for (int k = 0; k < P::NC; ++k) x[k] = xp[k];
@@ -505,6 +545,7 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
     double h = sa.tuner ? p.load_scalar(a.st.t_step) : sa.drift_step;
     int32_t n_acc = sa.tuner ? p.load_t(a.st.t_acc) : 0;
     int32_t n_prop = sa.tuner ? p.load_t(a.st.t_prop) : 0;
+    AcceptDraw<P> ad;
 
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
@@ -535,7 +576,7 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
         }
         qb = p.reduce(qb);
         const double ratio = ((lpp + qb) - lp) - qf;            // MALA.jl:107
-        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+        const bool acc = ad.test(p, rs, chain, i, t, ratio);
         if (acc) {
 #pragma unroll
             for (int k = 0; k < P::NC; ++k) x[k] = xp[k];

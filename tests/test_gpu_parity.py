@@ -53,7 +53,7 @@ def _dev_math(op, x, y=None):
 @pytest.mark.parametrize("op,name", [(0, "log"), (1, "exp"), (2, "sin2pi"), (3, "cos2pi"), (4, "sqrt"),
                                      (5, "div"), (7, "round"), (9, "bm_log_u32"), (10, "sin2pi_u32"),
                                      (11, "cos2pi_u32"), (12, "sqrt_pos_normal"), (13, "exp_tab"),
-                                     (14, "log_tab")])
+                                     (14, "log_tab"), (16, "bm_rad2_u32")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -69,7 +69,7 @@ def test_device_detmath_bitwise(gpu, op, name):
                             -2.0 * np.log((np.arange(0, 4000) + 0.5) * 2.0**-32),
                             -2.0 * np.log((2.0**32 - 0.5 - np.arange(0, 4000)) * 2.0**-32),
                             np.nextafter(np.arange(1.0, 47.0) ** 2, 0), np.arange(1.0, 47.0) ** 2])
-    elif op in (9, 10, 11):      # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
+    elif op in (9, 10, 11, 16):  # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
         x = np.concatenate([np.floor(rng.uniform(0, 2**32, 200000)), np.arange(0, 2000),
                             2.0**32 - 1 - np.arange(0, 2000), (np.arange(-40, 40) + 2**29 * np.arange(1, 8)[:, None]
                                                                ).ravel() % 2**32])
