@@ -280,6 +280,71 @@ __device__ __forceinline__ double bm_rad2_u32(uint32_t w, const double (*tab)[4]
     return hi + lo;
 }
 
+// The Box-Muller radius sqrt(-2 log u) as a polynomial (round 3; scripts/gen_bm_log_table.py BM_RADP / BM_RADT):
+// side = w >> 31 folds u >= 1/2 onto 1 - u = (~w + 1/2) 2^-32 (exact), so both halves are x 2^-32 with x = v + 1/2
+// in [1/2, 2^31); the binade e of x and the top 5 mantissa bits k pick a degree-7 polynomial in the exact residual
+// t = m - (1 + (2k+1)/64), |t| <= 1/64 (a0 as hi + lo, a5..a7 as floats).  <= 0.51 ulp; 20 VALU operations against
+// 32 for the log and the IEEE sqrt.  Binades 21..30 (kBmRadPdTab / kBmRadPfTab, the table a kernel may stage into
+// LDS) hold all but 2^-11 of the draws; x < 2^21 re-reads its coefficients from the global tail table (binades
+// -1..20) on the lanes that need it -- four loads under a branch a wave takes with probability 3% per radius, the
+// polynomial itself shared.  The three double chunks of a row are stored chunk-major (row i's chunk j at
+// j * NROWS + i), so one chunk's gathers spread over the LDS banks; the float quadruple is a fourth 16-byte gather.
+static __device__ const double kBmRadPdTab[3 * BM_RADP_NROWS][2] = {BM_RADPD_TABLE_ROWS};
+static __device__ const float kBmRadPfTab[BM_RADP_NROWS][4] = {BM_RADPF_TABLE_ROWS};
+static __device__ const double kBmRadTdTab[3 * BM_RADT_NROWS][2] = {BM_RADTD_TABLE_ROWS};
+static __device__ const float kBmRadTfTab[BM_RADT_NROWS][4] = {BM_RADTF_TABLE_ROWS};
+
+struct RadTab {                      // the radius polynomial table: a kernel's LDS copy or the global one
+    const double (*d)[2];
+    const float (*f)[4];
+};
+__device__ __forceinline__ RadTab rad_tab_global() { return RadTab{kBmRadPdTab, kBmRadPfTab}; }
+
+__device__ __forceinline__ double bm_radius_u32(uint32_t w, RadTab rt) {
+    typedef double f64x2_t __attribute__((ext_vector_type(2)));
+    typedef float f32x4_t __attribute__((ext_vector_type(4)));
+    const uint32_t side = w >> 31;
+    const uint32_t v = w ^ (0u - side);
+    const double x = (double)v + 0.5;                                   // exact
+    const uint64_t b = d2bits(x);
+    const uint32_t xh = (uint32_t)(b >> 32);
+    const bool tail = v < (1u << 21);
+    // row = side * NROWS/2 + (e - 21) * 32 + k = (xh >> 15) - ((1023 + 21) << 5) + side * NROWS/2 (0 on the tail)
+    int row = (int)(xh >> 15) - ((1023 + 21) << 5) + (int)side * (BM_RADP_NROWS / 2);
+    row = tail ? 0 : row;
+    const double t = bits2d(((uint64_t)((xh & 0x7fffu) | 0x3ff00000u) << 32) | (b & 0xffffffffull)) -
+                     (1.0 + 1.0 / 64.0);                                // exact (Sterbenz)
+    f64x2_t c0 = *reinterpret_cast<const f64x2_t*>(rt.d[row]);                       // a0_hi, a0_lo
+    f64x2_t c1 = *reinterpret_cast<const f64x2_t*>(rt.d[BM_RADP_NROWS + row]);       // a1, a2
+    f64x2_t c2 = *reinterpret_cast<const f64x2_t*>(rt.d[2 * BM_RADP_NROWS + row]);   // a3, a4
+    f32x4_t cf = *reinterpret_cast<const f32x4_t*>(rt.f[row]);                       // a5, a6, a7
+    if (tail) {
+        // explicit loads: as plain C++ the compiler merges them with the main-table loads above into one load through
+        // a selected pointer (flat, 64-bit addresses on every lane of every radius)
+        const uint32_t rw = (uint32_t)((int)(xh >> 15) - ((1023 - 1) << 5) + (int)side * (BM_RADT_NROWS / 2)) * 16u;
+        asm volatile(
+            "global_load_dwordx4 %0, %4, %8\n\t"
+            "global_load_dwordx4 %1, %5, %8\n\t"
+            "global_load_dwordx4 %2, %6, %8\n\t"
+            "global_load_dwordx4 %3, %7, %9\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(cf)
+            : "v"(rw), "v"(rw + 16u * BM_RADT_NROWS), "v"(rw + 32u * BM_RADT_NROWS), "v"(rw), "s"(&kBmRadTdTab[0][0]),
+              "s"(&kBmRadTfTab[0][0])
+            : "memory");
+    }
+    double q = __builtin_fma((double)cf.z, t, (double)cf.y);
+    q = __builtin_fma(q, t, (double)cf.x);
+    q = __builtin_fma(q, t, c2.y);
+    q = __builtin_fma(q, t, c2.x);
+    q = __builtin_fma(q, t, c1.y);
+    q = __builtin_fma(q, t, c1.x);
+    q = __builtin_fma(q, t, c0.y);
+    double r = q + c0.x;
+    asm volatile("" : "+v"(r));     // computed here: not sunk past the next radius's branch with its coefficients live
+    return r;
+}
+
 typedef double dm_f64x2 __attribute__((ext_vector_type(2)));
 
 // exp for the logistic likelihood (prob = 1/(1+exp(-X*vars)), examples/logistic_regression.jl:19), table-
@@ -440,22 +505,23 @@ __device__ __forceinline__ double sqrt_pos_normal(double x) {
 
 // Two Box-Muller pairs from one Philox block: radius sqrt(-2 log u1), u1 = (w.x + 1/2) 2^-32 in (0,1);
 // angle 2 pi u2, u2 = w.y 2^-32.
-// tab, sct: the radius^2 (bm_rad2_u32) and angle tables, in global memory (default) or a kernel's LDS copies
+// rt, sct: the radius polynomial (bm_radius_u32) and angle tables, in global memory (default) or a kernel's LDS copies
 __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1, double& z2, double& z3,
-                                         const double (*tab)[4] = kBmRad512Tab,
+                                         RadTab rt = rad_tab_global(),
                                          const double (*sct)[2] = kBmSinCos1024Tab) {
     {
-        const double rad = sqrt_pos_normal(bm_rad2_u32(w.x, tab));
+        const double rad = bm_radius_u32(w.x, rt);
         double s, c;
         det_sincos2pi_u32(w.y, s, c, sct);
         z0 = rad * c; z1 = rad * s;
     }
     {
-        const double rad = sqrt_pos_normal(bm_rad2_u32(w.z, tab));
+        const double rad = bm_radius_u32(w.z, rt);
         double s, c;
         det_sincos2pi_u32(w.w, s, c, sct);
         z2 = rad * c; z3 = rad * s;
     }
+    asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));   // likewise the products
 }
 
 // ratio > det_log(u), exactly (the RWM / MALA test `ratio > log(rand())`, RWM.jl:63, MALA.jl:108).  A

@@ -7,12 +7,13 @@
 
 namespace mcmc {
 
-#ifndef LPC_MINW
-#define LPC_MINW 2
-#endif
-// F: d == 4 NB (LaneChain FULL); US: uniform RWM scale
+// F: d == 4 NB (LaneChain FULL); US: uniform RWM scale.  RWM (config 2, d = 3): 768-thread blocks reading the
+// Box-Muller tables from LDS (56 KB a block: two blocks, six waves per SIMD); MALA / HMC read them from global memory
+constexpr int kLpcRwmThreads = 768;
 template <int NB, bool F, class M, bool US>
-__global__ __launch_bounds__(kBlock, LPC_MINW) void lpc_rwm(KernelArgs a) { rwm_body<LaneChain<NB, F>, M, US>(a); }
+__global__ __launch_bounds__(kLpcRwmThreads) void lpc_rwm(KernelArgs a) {
+    rwm_body<LaneChain<NB, F, false, kLpcRwmThreads, kTabLds>, M, US>(a);
+}
 template <int NB, bool F, class M>
 __global__ __launch_bounds__(kBlock, 2) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
 template <int NB, bool F, class M, bool DA>
@@ -24,19 +25,27 @@ __global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* x
 }
 
 // 16 < d <= 32: two lanes per chain (samplers.hpp PairChain), NB Philox blocks per lane; four waves per SIMD
-// Waves per SIMD (the launch bound): RWM holds x and the proposal, 16 coordinates each, in 128 VGPRs (4 waves; 3
-// when d < 2 NC leaves per-coordinate masks live); MALA 3 (2 with masks); HMC's x0, x, momentum and carried kicks
-// need ~240 (2 waves, where the lane-per-chain d = 32 kernel fitted one)
+// Waves per SIMD (the launch bound) and block size: RWM holds x and the proposal, 16 coordinates each, in 128 VGPRs
+// (4 waves: two 512-thread blocks of 56 KB LDS; 3 when d < 2 NC leaves per-coordinate masks live); MALA 3 (one
+// 768-thread block; 2 with masks); HMC's x0, x, momentum and carried kicks need ~220 (2 waves, where the lane-per-
+// chain d = 32 kernel fitted one).  The Box-Muller tables are read from LDS.  MALA's block sizes, measured (r3g, d = 32,
+// 2^20 chains): 768 threads / LDS tables 0.0957 ms a step, 512 / LDS (two waves) 0.0966, 256 / global tables 0.1031.
+template <int NB, bool F>
+constexpr int lpp_mala_threads() { return F ? 768 : 512; }
 template <int NB, bool F, class M, bool US>
-__global__ __launch_bounds__(kBlock, F && US ? 4 : 3) void lpp_rwm(KernelArgs a) { rwm_body<PairChain<NB, F>, M, US>(a); }
+__global__ __launch_bounds__(512, F && US ? 4 : 3) void lpp_rwm(KernelArgs a) {
+    rwm_body<PairChain<NB, F, 512, kTabLds>, M, US>(a);
+}
 template <int NB, bool F, class M>
-__global__ __launch_bounds__(kBlock, F ? 3 : 2) void lpp_mala(KernelArgs a) { mala_body<PairChain<NB, F>, M>(a); }
+__global__ __launch_bounds__((lpp_mala_threads<NB, F>()), F ? 3 : 2) void lpp_mala(KernelArgs a) {
+    mala_body<PairChain<NB, F, lpp_mala_threads<NB, F>(), kTabLds>, M>(a);
+}
 template <int NB, bool F, class M, bool DA>
-__global__ __launch_bounds__(kBlock, 2) void lpp_hmc(KernelArgs a) { hmc_body<PairChain<NB, F>, M, DA>(a); }
+__global__ __launch_bounds__(512, 2) void lpp_hmc(KernelArgs a) { hmc_body<PairChain<NB, F, 512, kTabLds>, M, DA>(a); }
 template <int NB, class M>
 __global__ __launch_bounds__(kBlock) void lpp_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {
-    eval_body<PairChain<NB>, M>(a, xin, lp, g, check);
+    eval_body<PairChain<NB, false, kBlock, kTabGlobal>, M>(a, xin, lp, g, check);
 }
 
 // RWM for a handful of chains (C <= 64; config 1 is one chain), where one lane per chain leaves the chip idle
@@ -319,26 +328,27 @@ static void lpc_spec_launch(const KernelArgs& a, hipStream_t st) {
 // 16 < d <= 32 (NB = ceil(d/4) > 4): the two-lanes-per-chain kernels, NBL = ceil(NB / 2) blocks per lane
 template <int NBL, bool F, class M>
 static hipError_t lpp_launch(const KernelArgs& a, hipStream_t st) {
-    const dim3 grid((unsigned)((a.s.C + PairChain<NBL>::kChainsPerBlock - 1) / PairChain<NBL>::kChainsPerBlock));
+    auto grid = [&](int threads) { return dim3((unsigned)((a.s.C + threads / 2 - 1) / (threads / 2))); };
     const char* b = F ? "true" : "false";
     const char* us = a.s.scale_uniform ? "true" : "false";
+    constexpr int TM = lpp_mala_threads<NBL, F>();
     switch (a.sa.kind) {
         case SK_RWM:
             mcmc_note_step_kernel("lpp_rwm<%d, %s, %s, %s>", NBL, b, M::kName, us);
-            if (a.s.scale_uniform) lpp_rwm<NBL, F, M, true><<<grid, kBlock, 0, st>>>(a);
-            else lpp_rwm<NBL, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            if (a.s.scale_uniform) lpp_rwm<NBL, F, M, true><<<grid(512), 512, 0, st>>>(a);
+            else lpp_rwm<NBL, F, M, false><<<grid(512), 512, 0, st>>>(a);
             break;
         case SK_MALA:
             mcmc_note_step_kernel("lpp_mala<%d, %s, %s>", NBL, b, M::kName);
-            lpp_mala<NBL, F, M><<<grid, kBlock, 0, st>>>(a);
+            lpp_mala<NBL, F, M><<<grid(TM), TM, 0, st>>>(a);
             break;
         case SK_HMC:
             mcmc_note_step_kernel("lpp_hmc<%d, %s, %s, false>", NBL, b, M::kName);
-            lpp_hmc<NBL, F, M, false><<<grid, kBlock, 0, st>>>(a);
+            lpp_hmc<NBL, F, M, false><<<grid(512), 512, 0, st>>>(a);
             break;
         case SK_HMCDA:
             mcmc_note_step_kernel("lpp_hmc<%d, %s, %s, true>", NBL, b, M::kName);
-            lpp_hmc<NBL, F, M, true><<<grid, kBlock, 0, st>>>(a);
+            lpp_hmc<NBL, F, M, true><<<grid(512), 512, 0, st>>>(a);
             break;
         default: return hipErrorInvalidValue;
     }
@@ -376,8 +386,11 @@ static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
                     break;
                 }
                 mcmc_note_step_kernel("lpc_rwm<%d, %s, %s, %s>", NB, b, M::kName, us);
-                if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
-                else lpc_rwm<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+                {
+                    const dim3 g768((unsigned)((a.s.C + kLpcRwmThreads - 1) / kLpcRwmThreads));
+                    if (a.s.scale_uniform) lpc_rwm<NB, F, M, true><<<g768, kLpcRwmThreads, 0, st>>>(a);
+                    else lpc_rwm<NB, F, M, false><<<g768, kLpcRwmThreads, 0, st>>>(a);
+                }
                 break;
             case SK_MALA:
                 mcmc_note_step_kernel("lpc_mala<%d, %s, %s>", NB, b, M::kName);
@@ -443,7 +456,9 @@ template <int NB, class M, bool DA>
 __global__ __launch_bounds__(kBlock) void lpc_hmc_rec(KernelArgs a, LeapRec r) { hmc_record_body<LaneChain<NB>, M, DA>(a, r); }
 
 template <int NB, class M, bool DA>
-__global__ __launch_bounds__(kBlock) void lpp_hmc_rec(KernelArgs a, LeapRec r) { hmc_record_body<PairChain<NB>, M, DA>(a, r); }
+__global__ __launch_bounds__(kBlock) void lpp_hmc_rec(KernelArgs a, LeapRec r) {
+    hmc_record_body<PairChain<NB, false, kBlock, kTabGlobal>, M, DA>(a, r);
+}
 
 template <class M>
 static hipError_t lpc_record_m(const KernelArgs& a, const LeapRec& r, hipStream_t st) {

@@ -88,6 +88,7 @@ __global__ void k_detmath(int op, int64_t n, const double* x, const double* y, d
         case 14: r = det_log_tab(a); break;
         case 15: r = gt_det_log(a, y[i]) ? 1.0 : 0.0; break;      // the screened accept test: a > det_log(y)
         case 16: r = bm_rad2_u32((uint32_t)(uint64_t)a); break;    // the Box-Muller radius^2, -2 log u
+        case 17: r = bm_radius_u32((uint32_t)(uint64_t)a, rad_tab_global()); break;   // the radius polynomial
         default: r = 0.0;
     }
     out[i] = r;

@@ -10,13 +10,19 @@ namespace mcmc {
 
 constexpr int kChainsPerBlock = kBlock / 64;
 
-// F: d == 256 NB (WaveChain FULL)
+// F: d == 256 NB (WaveChain FULL).  The Box-Muller tables: from LDS for NB >= 4 (two waves per SIMD anyway by their
+// registers, so two 56 KB blocks per CU cost nothing; config 4 is NB = 4), from global memory for NB <= 2 (three or
+// four waves per SIMD, which 56 KB blocks would cut to two)
+template <int NB>
+constexpr int wpc_tab() { return NB >= 4 ? kTabLds : kTabGlobal; }
 template <int NB, bool F, class M>
-__global__ __launch_bounds__(kBlock) void wpc_rwm(KernelArgs a) { rwm_body<WaveChain<NB, F>, M>(a); }
+__global__ __launch_bounds__(kBlock) void wpc_rwm(KernelArgs a) { rwm_body<WaveChain<NB, F, 1, wpc_tab<NB>()>, M>(a); }
 template <int NB, bool F, class M>
-__global__ __launch_bounds__(kBlock) void wpc_mala(KernelArgs a) { mala_body<WaveChain<NB, F>, M>(a); }
+__global__ __launch_bounds__(kBlock) void wpc_mala(KernelArgs a) { mala_body<WaveChain<NB, F, 1, wpc_tab<NB>()>, M>(a); }
 template <int NB, bool F, class M, bool DA>
-__global__ __launch_bounds__(kBlock) void wpc_hmc(KernelArgs a) { hmc_body<WaveChain<NB, F>, M, DA>(a); }
+__global__ __launch_bounds__(kBlock) void wpc_hmc(KernelArgs a) {
+    hmc_body<WaveChain<NB, F, 1, wpc_tab<NB>()>, M, DA>(a);
+}
 template <int NB, class M>
 __global__ __launch_bounds__(kBlock) void wpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {
@@ -25,11 +31,11 @@ __global__ __launch_bounds__(kBlock) void wpc_eval(KernelArgs a, const double* x
 
 // block per chain, d > 2048: W waves hold the chain's coordinates (WaveChain<8, false, W>), one chain per block
 template <int W, class M>
-__global__ __launch_bounds__(64 * W) void bpc_rwm(KernelArgs a) { rwm_body<WaveChain<8, false, W>, M>(a); }
+__global__ __launch_bounds__(64 * W) void bpc_rwm(KernelArgs a) { rwm_body<WaveChain<8, false, W, kTabLds>, M>(a); }
 template <int W, class M>
-__global__ __launch_bounds__(64 * W) void bpc_mala(KernelArgs a) { mala_body<WaveChain<8, false, W>, M>(a); }
+__global__ __launch_bounds__(64 * W) void bpc_mala(KernelArgs a) { mala_body<WaveChain<8, false, W, kTabLds>, M>(a); }
 template <int W, class M, bool DA>
-__global__ __launch_bounds__(64 * W) void bpc_hmc(KernelArgs a) { hmc_body<WaveChain<8, false, W>, M, DA>(a); }
+__global__ __launch_bounds__(64 * W) void bpc_hmc(KernelArgs a) { hmc_body<WaveChain<8, false, W, kTabLds>, M, DA>(a); }
 template <int W, class M>
 __global__ __launch_bounds__(64 * W) void bpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {

@@ -33,36 +33,79 @@ namespace mcmc {
 
 constexpr int kBlock = 256;
 
-// The Box-Muller tables (32 KB) into a block's LDS: every 16-byte load in flight before the first store (a loop
-// of load-store pairs costs one L2 round trip per iteration), then one barrier.  NT threads (kBlock, or the
-// block-per-chain kernels' 64 W).
-template <int NT = kBlock>
-__device__ __forceinline__ void stage_bm_tables(double (*lt)[4], double (*ls)[2]) {
+// Where a kernel reads the Box-Muller tables (the radius polynomials of bm_radius_u32 and the angle table):
+//   kTabLds     staged once per block into LDS (56 KB: the hot kernels -- their per-lane row gathers go to LDS);
+//   kTabGlobal  straight from global memory (L1 / L2), for kernels whose occupancy 56 KB per block would cut or
+//               whose LDS is taken (the few-chain kernels, RAM, the diagnostics); the same values either way.
+enum TabMode : int { kTabLds = 0, kTabGlobal = 1 };
+
+struct BmLds {
+    double (*rd)[2];
+    float (*rf)[4];
+    double (*sc)[2];
+};
+// The block's LDS copies (one allocation per kernel, whoever asks)
+__device__ __forceinline__ BmLds bm_lds_tables() {
+    __shared__ __attribute__((aligned(16))) double lds_radd[3 * BM_RADP_NROWS][2];
+    __shared__ __attribute__((aligned(16))) float lds_radf[BM_RADP_NROWS][4];
+    __shared__ __attribute__((aligned(16))) double lds_sct[1024][2];
+    return BmLds{lds_radd, lds_radf, lds_sct};
+}
+
+// The tables into a block's LDS by its NT threads: every 16-byte load of a batch in flight before its first store
+// (a loop of load-store pairs costs one L2 round trip per iteration), then one barrier.
+template <int NT>
+__device__ __forceinline__ void stage_bm_tables(const BmLds& L) {
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    constexpr int kN = 1024 / NT;                           // 16-byte rows per thread per table
-    const f64x2_t* gt = reinterpret_cast<const f64x2_t*>(&kBmRad512Tab[0][0]);
+    constexpr int kD = 3 * BM_RADP_NROWS, kF = BM_RADP_NROWS, kS = 1024;     // 16-byte units of each table
+    constexpr int kU = kD + kF + kS;
+    constexpr int kN = (kU + NT - 1) / NT;
+    constexpr int kBatch = 8;
+    const f64x2_t* gd = reinterpret_cast<const f64x2_t*>(&kBmRadPdTab[0][0]);
+    const f64x2_t* gf = reinterpret_cast<const f64x2_t*>(&kBmRadPfTab[0][0]);
     const f64x2_t* gs = reinterpret_cast<const f64x2_t*>(&kBmSinCos1024Tab[0][0]);
-    f64x2_t a[kN], b[kN];
+    f64x2_t* ld = reinterpret_cast<f64x2_t*>(&L.rd[0][0]);
+    f64x2_t* lf = reinterpret_cast<f64x2_t*>(&L.rf[0][0]);
+    f64x2_t* ls = reinterpret_cast<f64x2_t*>(&L.sc[0][0]);
 #pragma unroll
-    for (int j = 0; j < kN; ++j) {
-        a[j] = gt[threadIdx.x + NT * j];
-        b[j] = gs[threadIdx.x + NT * j];
-    }
+    for (int j0 = 0; j0 < kN; j0 += kBatch) {
+        f64x2_t v[kBatch];
 #pragma unroll
-    for (int j = 0; j < kN; ++j) {
-        reinterpret_cast<f64x2_t*>(&lt[0][0])[threadIdx.x + NT * j] = a[j];
-        reinterpret_cast<f64x2_t*>(&ls[0][0])[threadIdx.x + NT * j] = b[j];
+        for (int j = j0; j < j0 + kBatch && j < kN; ++j) {
+            const int u = (int)threadIdx.x + NT * j;
+            if (u < kU) v[j - j0] = u < kD ? gd[u] : (u < kD + kF ? gf[u - kD] : gs[u - kD - kF]);
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + kBatch && j < kN; ++j) {
+            const int u = (int)threadIdx.x + NT * j;
+            if (u < kD) ld[u] = v[j - j0];
+            else if (u < kD + kF) lf[u - kD] = v[j - j0];
+            else if (u < kU) ls[u - kD - kF] = v[j - j0];
+        }
     }
     __syncthreads();
 }
 
-// The block's LDS copies of the Box-Muller tables (one allocation per kernel, whoever asks)
-__device__ __forceinline__ void bm_lds_tables(const double (*&lt)[4], const double (*&ls)[2]) {
-    __shared__ __attribute__((aligned(16))) double lds_tab[512][4];
-    __shared__ __attribute__((aligned(16))) double lds_sct[1024][2];
-    lt = lds_tab;
-    ls = lds_sct;
-}
+// The tables a policy reads: LDS (staged by stage()) or global
+template <int TAB, int NT>
+struct BmTables {
+    RadTab rad;
+    const double (*sct)[2];
+    BmLds lds;
+    __device__ __forceinline__ void init() {
+        if constexpr (TAB == kTabLds) {
+            lds = bm_lds_tables();
+            rad = RadTab{lds.rd, lds.rf};
+            sct = lds.sc;
+        } else {
+            rad = rad_tab_global();
+            sct = kBmSinCos1024Tab;
+        }
+    }
+    __device__ __forceinline__ void stage() const {
+        if constexpr (TAB == kTabLds) stage_bm_tables<NT>(lds);
+    }
+};
 
 // ------------------------------------------------------------------ mappings
 // NB = ceil(d/4).  FULL: d == 4 NB, every register coordinate is a real one -- no validity masks
@@ -70,27 +113,28 @@ __device__ __forceinline__ void bm_lds_tables(const double (*&lt)[4], const doub
 // SPLIT: eval_lp sums in PairChain's order (coordinates of the first PairChain half, then the second, then the two
 // partial sums added) -- for the few-chain RWM kernel lpc_rwm_la, which runs the same chains as the 16 < d <= 32
 // PairChain kernels and must agree with them bit for bit
-template <int NB_, bool FULL = false, bool SPLIT = false>
+// TH: threads per block (chains per block); TAB: where the Box-Muller tables are read (TabMode)
+template <int NB_, bool FULL = false, bool SPLIT = false, int TH = kBlock, int TAB = kTabGlobal>
 struct LaneChain {
     static constexpr int NB = NB_;
     static constexpr int NC = 4 * NB_;
     static constexpr int kSplit = SPLIT ? 4 * ((NB_ + 1) / 2) : 0;
-    static constexpr int kChainsPerBlock = kBlock;
+    static constexpr int kThreads = TH;
+    static constexpr int kChainsPerBlock = TH;
     static constexpr bool kPairs = false;
     int64_t c;        // local chain index
     bool live;        // c < C
     int d;
-    const double (*tab)[4];   // LDS copies of the Box-Muller log and angle tables: per-lane row gathers
-    const double (*sct)[2];   // from LDS, not from the vector L1 (every block thread calls the constructor)
+    BmTables<TAB, TH> bt;     // the Box-Muller tables (every block thread calls the constructor)
     // defer: the caller issues its state loads first and then calls stage() (the two latencies overlap)
     __device__ LaneChain(const StepArgs& s, bool defer = false) {
-        c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        c = (int64_t)blockIdx.x * TH + threadIdx.x;
         live = c < s.C;
         d = s.d;
-        bm_lds_tables(tab, sct);
+        bt.init();
         if (!defer) stage();
     }
-    __device__ __forceinline__ void stage() const { stage_bm_tables(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct)); }
+    __device__ __forceinline__ void stage() const { bt.stage(); }
     __device__ __forceinline__ int coord(int k) const { return k; }
     // blocks 0..NB-2 are always full (NB = ceil(d/4)); only the last block's coordinates are tested
     __device__ __forceinline__ bool valid(int k) const { return FULL || k < 4 * (NB - 1) || k < d; }
@@ -169,28 +213,28 @@ struct LaneChain {
 // lane accumulates its coordinates left to right, then (half 0) + (half 1), formed identically in both lanes by
 // one v_permlane32_swap per dword (oracle order ORC_ORDER_PAIR).  Both lanes of a chain hold the same lp, ratio
 // and accept decision; memory: row k of the wave's 32 chains is one 256-byte run per half.
-template <int NB_, bool FULL = false>
+template <int NB_, bool FULL = false, int TH = 512, int TAB = kTabLds>
 struct PairChain {
     static constexpr int NB = NB_;
     static constexpr int NC = 4 * NB_;
-    static constexpr int kChainsPerBlock = kBlock / 2;
+    static constexpr int kThreads = TH;
+    static constexpr int kChainsPerBlock = TH / 2;
     static constexpr bool kPairs = true;
     int64_t c;        // local chain index
     bool live;
     int d;
     int h;            // half: 0 (lanes 0-31) or 1 (lanes 32-63)
-    const double (*tab)[4];
-    const double (*sct)[2];
+    BmTables<TAB, TH> bt;
     __device__ PairChain(const StepArgs& s, bool defer = false) {
         const int lane = (int)(threadIdx.x & 63);
         c = (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)(threadIdx.x >> 6) * 32 + (lane & 31);
         h = lane >> 5;
         live = c < s.C;
         d = s.d;
-        bm_lds_tables(tab, sct);
+        bt.init();
         if (!defer) stage();
     }
-    __device__ __forceinline__ void stage() const { stage_bm_tables(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct)); }
+    __device__ __forceinline__ void stage() const { bt.stage(); }
     __device__ __forceinline__ int coord(int k) const { return h * NC + k; }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(h * NB + b); }
@@ -305,7 +349,7 @@ __device__ __forceinline__ double block_sum(double v) {
 // runtime d they are 4 G lane masks live across the step loop, which spill the scalar file)
 // W > 1: one chain per block of W waves (d up to 256 G W; kernels/wpc_impl.hpp bpc_*): lane l of the 64 W owns
 // coordinates 4 (l + 64 W k) + e, sums per lane, per wave, then over the waves (block_sum, oracle order W)
-template <int G, bool FULL = false, int W = 1>
+template <int G, bool FULL = false, int W = 1, int TAB = kTabGlobal>
 struct WaveChain {
     static constexpr int NB = G;
     static constexpr int NC = 4 * G;
@@ -316,20 +360,17 @@ struct WaveChain {
     int d;
     int lane;
     int64_t ldr;      // row stride of chain-major state (multiple of 4)
-    const double (*tab)[4];   // LDS copies of the Box-Muller tables (as LaneChain)
-    const double (*sct)[2];
+    BmTables<TAB, W == 1 ? kBlock : 64 * W> bt;
     __device__ WaveChain(const StepArgs& s, bool defer = false) {
         c = W == 1 ? (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
         live = c < s.C;
         d = s.d;
         lane = W == 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
         ldr = s.ld;
-        bm_lds_tables(tab, sct);
+        bt.init();
         if (!defer) stage();
     }
-    __device__ __forceinline__ void stage() const {
-        stage_bm_tables<W == 1 ? kBlock : L>(const_cast<double (*)[4]>(tab), const_cast<double (*)[2]>(sct));
-    }
+    __device__ __forceinline__ void stage() const { bt.stage(); }
     __device__ __forceinline__ int coord(int k) const { return 4 * (lane + L * (k >> 2)) + (k & 3); }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + L * b); }
@@ -406,14 +447,15 @@ __device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32
 #pragma unroll
     for (int b = 0; b < P::NB; ++b) {
         const u32x4 w = rs.block(chain, step, p.block(b), TAG_NORMAL);
-        normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3], p.tab, p.sct);
+        normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3], p.bt.rad, p.bt.sct);
     }
 }
 
+
 template <class P>
 struct split_of { static constexpr int value = 0; };
-template <int NB, bool F, bool S>
-struct split_of<LaneChain<NB, F, S>> { static constexpr int value = LaneChain<NB, F, S>::kSplit; };
+template <int NB, bool F, bool S, int T, int TAB>
+struct split_of<LaneChain<NB, F, S, T, TAB>> { static constexpr int value = LaneChain<NB, F, S, T, TAB>::kSplit; };
 
 template <class P, class M>
 __device__ __forceinline__ double eval_lp(const P& p, const M& model, const double (&v)[P::NC], bool& oos) {
@@ -726,9 +768,13 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             bool big;
             lpl = trajectory_halfneg(p, model, eps, nl, x, m, big);
             if (big) {                                          // -2x overflowed somewhere: the exact path
+                // the same draw again, from a step index the compiler cannot see is i: otherwise it reuses the first
+                // draw's values and keeps them live across the trajectory (d = 1024 HMC: 214 -> 286 VGPRs)
+                uint32_t si = (uint32_t)i;
+                asm volatile("" : "+s"(si));
 #pragma unroll
                 for (int k = 0; k < P::NC; ++k) x[k] = x0[k];
-                gen_normals(p, rs, chain, (uint32_t)i, m);
+                gen_normals(p, rs, chain, si, m);
                 lpl = trajectory(p, model, eps, nl, x, m);
             }
         } else {
@@ -921,7 +967,7 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
         double un[NC], nzn = 0.0;
         auto zblock = [&](int b, double (&z4)[4]) {                           // step i + 1's rvec, block b
             const u32x4 w = rs.block(chain, (uint32_t)(i + 1), p.block(b), TAG_NORMAL);
-            normals4(w, z4[0], z4[1], z4[2], z4[3], p.tab, p.sct);
+            normals4(w, z4[0], z4[1], z4[2], z4[3], p.bt.rad, p.bt.sct);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (!p.valid(4 * b + e)) z4[e] = 0.0;

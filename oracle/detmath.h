@@ -17,6 +17,7 @@
  *   det_exp ........... Cody-Waite reduction + degree-13 Taylor (fma Horner)
  *   det_sincos2pi ..... exact quarter-turn reduction + Taylor polynomials in r
  *   Box-Muller angle .. 1024-row sin/cos table + short Taylor polynomials (orc_sincos2pi_u32)
+ *   Box-Muller radius . per-segment degree-7 polynomials of sqrt(-2 log u) (orc_bm_radius_u32)
  *   Box-Muller ........ normals from 32-bit uniforms, 4 normals per Philox block
  *
  * Compile with -ffp-contract=off: every fused multiply-add is an explicit fma();
@@ -297,10 +298,54 @@ static inline void orc_sincos2pi_u32(uint32_t w, double* s_out, double* c_out) {
     *c_out = ca + fma(-sa, sr, ca * cm1);
 }
 
+/* ------------------------------------------------------- Box-Muller radius */
+/* sqrt(-2 log((w + 0.5) 2^-32)) as a table of polynomials (scripts/gen_bm_log_table.py, BM_RADP / BM_RADT): side =
+   w >> 31 folds u >= 1/2 onto 1 - u = (~w + 0.5) 2^-32 (the same radius law, exact), so x = v + 0.5 in [1/2, 2^31);
+   the binade e of x and the top 5 mantissa bits k pick a row -- side * 320 + (e - 21) * 32 + k of the main table
+   for e = 21..30, side * 704 + (e + 1) * 32 + k of the tail table for e = -1..20 (v < 2^21) -- and the radius is a
+   degree-7 polynomial in the exact residual t = m - (1 + (2k+1)/64), |t| <= 1/64 (the mantissa with its top 5
+   bits cleared, less 1 + 1/64); a0 is a hi + lo pair, a5..a7 floats.  Device twin: bm_radius_u32
+   (csrc/detmath.hpp); the same operations in the same order, so the two agree bit for bit. */
+static const double orc_bm_radpd_tab[3 * BM_RADP_NROWS][2] = {BM_RADPD_TABLE_ROWS};
+static const float orc_bm_radpf_tab[BM_RADP_NROWS][4] = {BM_RADPF_TABLE_ROWS};
+static const double orc_bm_radtd_tab[3 * BM_RADT_NROWS][2] = {BM_RADTD_TABLE_ROWS};
+static const float orc_bm_radtf_tab[BM_RADT_NROWS][4] = {BM_RADTF_TABLE_ROWS};
+
+static inline double orc_bm_radius_u32(uint32_t w) {
+    uint32_t side = w >> 31;
+    uint32_t v = w ^ (0u - side);
+    double x = (double)v + 0.5;
+    uint64_t b = orc_d2bits(x);
+    uint32_t xh = (uint32_t)(b >> 32);
+    const double (*d)[2];
+    const float* cf;
+    int row, n;
+    if (v < (1u << 21)) {
+        row = (int)(xh >> 15) - ((1023 - 1) << 5) + (int)side * (BM_RADT_NROWS / 2);
+        d = orc_bm_radtd_tab; cf = orc_bm_radtf_tab[row]; n = BM_RADT_NROWS;
+    } else {
+        row = (int)(xh >> 15) - ((1023 + 21) << 5) + (int)side * (BM_RADP_NROWS / 2);
+        d = orc_bm_radpd_tab; cf = orc_bm_radpf_tab[row]; n = BM_RADP_NROWS;
+    }
+    double t = orc_bits2d(((uint64_t)((xh & 0x7fffu) | 0x3ff00000u) << 32) | (b & 0xffffffffull)) -
+               (1.0 + 1.0 / 64.0);
+    const double* c0 = d[row];
+    const double* c1 = d[n + row];
+    const double* c2 = d[2 * n + row];
+    double q = fma((double)cf[2], t, (double)cf[1]);
+    q = fma(q, t, (double)cf[0]);
+    q = fma(q, t, c2[1]);
+    q = fma(q, t, c2[0]);
+    q = fma(q, t, c1[1]);
+    q = fma(q, t, c1[0]);
+    q = fma(q, t, c0[1]);
+    return q + c0[0];
+}
+
 /* Four standard normals from one Philox block (two Box-Muller pairs). */
 static inline void orc_normals4(const uint32_t w[4], double z[4]) {
     for (int p = 0; p < 2; ++p) {
-        double rad = sqrt(-2.0 * orc_bm_log_u32(w[2 * p]));
+        double rad = orc_bm_radius_u32(w[2 * p]);
         double s, c;
         orc_sincos2pi_u32(w[2 * p + 1], &s, &c);
         z[2 * p] = rad * c;

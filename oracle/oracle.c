@@ -832,6 +832,7 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
             case 14: r = orc_log_tab(a); break;
             case 15: r = a > orc_log(y[i]) ? 1.0 : 0.0; break;    /* RWM.jl:63's test; device: gt_det_log */
             case 16: r = -2.0 * orc_bm_log_u32((uint32_t)(uint64_t)a); break;   /* device: bm_rad2_u32 */
+            case 17: r = orc_bm_radius_u32((uint32_t)(uint64_t)a); break;       /* device: bm_radius_u32 */
             case 8: {
                 uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
                 uint32_t key[2] = {0u, 0u}, w[4];

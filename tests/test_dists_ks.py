@@ -119,16 +119,20 @@ def test_ks_oracle(name, params, dist, which):
 
 def test_mala_lognormal_converges():
     """The SLOW case: the sup-distance between the pooled draws' cdf and LogNormal(-1, 1)'s falls as the run
-    grows (slow convergence of MALA(std) there, not a stationary bias)."""
+    grows (slow convergence of MALA(std) there, not a stationary bias): 10^4 -> 3 10^5 steps, averaged over two
+    seeds (one seed's ratio ranges 0.64-0.77 over seeds 1-4)."""
     name, params, dist = CASES[15]
     assert (name, params) == ("LogNormal", (-1, 1))
     _, sd = mean_std(dist)
     m = case_model(name, params, dist)
     D = []
-    for steps in (10000, 100000):
-        oc = orc.OracleChains(m, sampler_for("MALA", sd), nchains=64, seed=1)
-        s, _, _ = oc.run(mc.SerialMC(steps=steps, burnin=999, thinning=100))
-        D.append(ks_value(s[:, 0, :], dist) / math.sqrt(s[:, 0, :].size))
+    for steps in (10000, 300000):
+        d = 0.0
+        for seed in (1, 2):
+            oc = orc.OracleChains(m, sampler_for("MALA", sd), nchains=64, seed=seed)
+            s, _, _ = oc.run(mc.SerialMC(steps=steps, burnin=999, thinning=100))
+            d += ks_value(s[:, 0, :], dist) / math.sqrt(s[:, 0, :].size) / 2
+        D.append(d)
     assert D[1] < 0.85 * D[0], D
 
 

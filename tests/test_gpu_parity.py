@@ -53,7 +53,8 @@ def _dev_math(op, x, y=None):
 @pytest.mark.parametrize("op,name", [(0, "log"), (1, "exp"), (2, "sin2pi"), (3, "cos2pi"), (4, "sqrt"),
                                      (5, "div"), (7, "round"), (9, "bm_log_u32"), (10, "sin2pi_u32"),
                                      (11, "cos2pi_u32"), (12, "sqrt_pos_normal"), (13, "exp_tab"),
-                                     (14, "log_tab"), (16, "bm_rad2_u32")])
+                                     (14, "log_tab"), (16, "bm_rad2_u32"),
+                                     (17, "bm_radius_u32")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -69,10 +70,15 @@ def test_device_detmath_bitwise(gpu, op, name):
                             -2.0 * np.log((np.arange(0, 4000) + 0.5) * 2.0**-32),
                             -2.0 * np.log((2.0**32 - 0.5 - np.arange(0, 4000)) * 2.0**-32),
                             np.nextafter(np.arange(1.0, 47.0) ** 2, 0), np.arange(1.0, 47.0) ** 2])
-    elif op in (9, 10, 11, 16):  # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
+    elif op in (9, 10, 11, 16, 17):  # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
         x = np.concatenate([np.floor(rng.uniform(0, 2**32, 200000)), np.arange(0, 2000),
                             2.0**32 - 1 - np.arange(0, 2000), (np.arange(-40, 40) + 2**29 * np.arange(1, 8)[:, None]
                                                                ).ravel() % 2**32])
+        if op == 17:             # every polynomial segment's two ends on both sides, and the tail's edge (v = 2^21)
+            e, k = np.meshgrid(np.arange(21, 31), np.arange(32))
+            v = (2.0**e * (1 + k / 32)).ravel().astype(np.int64)
+            v = np.concatenate([v - 2, v - 1, v, v + 1, [2**21 - 2, 2**21 - 1, 2**21, 2**21 + 1, 2**31 - 1]])
+            x = np.concatenate([x, v, 2**32 - 1 - v]).astype(np.float64)
     elif op == 13:
         x = np.concatenate([rng.uniform(-750, 712, 200000), rng.uniform(-40, 40, 200000),
                             [0.0, np.inf, -np.inf, np.nan, 710.0, -746.0, -745.2, 709.79]])
