@@ -282,65 +282,78 @@ __device__ __forceinline__ double bm_rad2_u32(uint32_t w, const double (*tab)[4]
 
 // The Box-Muller radius sqrt(-2 log u) as a polynomial (round 3; scripts/gen_bm_log_table.py BM_RADP / BM_RADT):
 // side = w >> 31 folds u >= 1/2 onto 1 - u = (~w + 1/2) 2^-32 (exact), so both halves are x 2^-32 with x = v + 1/2
-// in [1/2, 2^31); the binade e of x and the top 5 mantissa bits k pick a degree-7 polynomial in the exact residual
-// t = m - (1 + (2k+1)/64), |t| <= 1/64 (a0 as hi + lo, a5..a7 as floats).  <= 0.51 ulp; 20 VALU operations against
-// 32 for the log and the IEEE sqrt.  Binades 21..30 (kBmRadPdTab / kBmRadPfTab, the table a kernel may stage into
-// LDS) hold all but 2^-11 of the draws; x < 2^21 re-reads its coefficients from the global tail table (binades
-// -1..20) on the lanes that need it -- four loads under a branch a wave takes with probability 3% per radius, the
-// polynomial itself shared.  The three double chunks of a row are stored chunk-major (row i's chunk j at
-// j * NROWS + i), so one chunk's gathers spread over the LDS banks; the float quadruple is a fourth 16-byte gather.
-static __device__ const double kBmRadPdTab[3 * BM_RADP_NROWS][2] = {BM_RADPD_TABLE_ROWS};
-static __device__ const float kBmRadPfTab[BM_RADP_NROWS][4] = {BM_RADPF_TABLE_ROWS};
-static __device__ const double kBmRadTdTab[3 * BM_RADT_NROWS][2] = {BM_RADTD_TABLE_ROWS};
-static __device__ const float kBmRadTfTab[BM_RADT_NROWS][4] = {BM_RADTF_TABLE_ROWS};
+// in [1/2, 2^31).  v >= 2^21 (all but 2^-11 of the draws): the binade e = 21..30 and top 5 mantissa bits k of v
+// pick a degree-7 polynomial in the exact residual t = m - (1 + (2k+1)/64), |t| <= 1/64, of v's mantissa (the 1/2
+// is inside the polynomial, so x is never formed); kBmRadPTab, the table a kernel may stage into LDS, rows chunk-
+// major (row i's chunk j -- (a0, a1), (a2, a3), (a4, a5), (a6, a7) -- at j * NROWS + i, so a wave's gathers of one
+// chunk spread over the LDS banks).  v < 2^21 re-reads its coefficients and residual from the global tail table
+// (binades -1..20 of x itself) on the lanes that need it: four loads under a branch a wave takes with probability
+// 3% per radius, the polynomial itself shared.  <= 1 ulp (1.4 ulp on the few segments whose radius crosses a power
+// of two: a0 is one double); 16 VALU operations against 32 for a log and an IEEE sqrt.
+static __device__ const double kBmRadPTab[4 * BM_RADP_NROWS][2] = {BM_RADP_TABLE_ROWS};
+static __device__ const double kBmRadTTab[4 * BM_RADT_NROWS][2] = {BM_RADT_TABLE_ROWS};
 
 struct RadTab {                      // the radius polynomial table: a kernel's LDS copy or the global one
     const double (*d)[2];
-    const float (*f)[4];
+    bool lds;                        // LDS: an out-of-range row (the tail lanes') reads harmlessly; global: clamped
 };
-__device__ __forceinline__ RadTab rad_tab_global() { return RadTab{kBmRadPdTab, kBmRadPfTab}; }
+__device__ __forceinline__ RadTab rad_tab_global() { return RadTab{kBmRadPTab, false}; }
 
 __device__ __forceinline__ double bm_radius_u32(uint32_t w, RadTab rt) {
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    typedef float f32x4_t __attribute__((ext_vector_type(4)));
-    const uint32_t side = w >> 31;
-    const uint32_t v = w ^ (0u - side);
-    const double x = (double)v + 0.5;                                   // exact
-    const uint64_t b = d2bits(x);
-    const uint32_t xh = (uint32_t)(b >> 32);
+    const uint32_t sm = (uint32_t)((int32_t)w >> 31);                   // side mask
+    const uint32_t v = w ^ sm;
+    const double y = (double)v;                                         // exact
+    const uint64_t b = d2bits(y);
+    const uint32_t yh = (uint32_t)(b >> 32);
     const bool tail = v < (1u << 21);
-    // row = side * NROWS/2 + (e - 21) * 32 + k = (xh >> 15) - ((1023 + 21) << 5) + side * NROWS/2 (0 on the tail)
-    int row = (int)(xh >> 15) - ((1023 + 21) << 5) + (int)side * (BM_RADP_NROWS / 2);
-    row = tail ? 0 : row;
-    const double t = bits2d(((uint64_t)((xh & 0x7fffu) | 0x3ff00000u) << 32) | (b & 0xffffffffull)) -
-                     (1.0 + 1.0 / 64.0);                                // exact (Sterbenz)
-    f64x2_t c0 = *reinterpret_cast<const f64x2_t*>(rt.d[row]);                       // a0_hi, a0_lo
-    f64x2_t c1 = *reinterpret_cast<const f64x2_t*>(rt.d[BM_RADP_NROWS + row]);       // a1, a2
-    f64x2_t c2 = *reinterpret_cast<const f64x2_t*>(rt.d[2 * BM_RADP_NROWS + row]);   // a3, a4
-    f32x4_t cf = *reinterpret_cast<const f32x4_t*>(rt.f[row]);                       // a5, a6, a7
+    // byte offset of row (yh >> 15) - ((1023 + 21) << 5) + side * NROWS/2 (yh >> 15 = biased exponent, k)
+    constexpr uint32_t kOff0 = 0u - ((uint32_t)((1023 + 21) << 5) << 4);
+    constexpr uint32_t kOff1 = kOff0 + (uint32_t)(BM_RADP_NROWS / 2) * 16u;
+    // the side select as one v_bfi_b32, the offset as one v_lshl_add_u32 and the residual's high word as one
+    // v_and_or_b32: the compiler spends two instructions on each (VOP3 takes no literal on gfx9)
+    uint32_t sel;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(sel) : "v"(sm), "v"(kOff1), "s"(kOff0));
+    uint32_t off;
+    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(off) : "v"(yh >> 15), "v"(sel));   // ((yh >> 15) << 4) + sel
+    uint32_t th = yh;                                                   // in place: y's high word is dead now
+    asm("v_and_or_b32 %0, %0, %1, %2" : "+v"(th) : "s"(0x7fffu), "v"(0x3ff00000u));
+    if (!rt.lds) off = tail ? 0u : off;
+    double t = bits2d(((uint64_t)th << 32) | (b & 0xffffffffull)) - (1.0 + 1.0 / 64.0);     // exact (Sterbenz)
+    const char* base = reinterpret_cast<const char*>(rt.d) + off;
+    f64x2_t c0 = *reinterpret_cast<const f64x2_t*>(base);
+    f64x2_t c1 = *reinterpret_cast<const f64x2_t*>(base + 16 * BM_RADP_NROWS);
+    f64x2_t c2 = *reinterpret_cast<const f64x2_t*>(base + 32 * BM_RADP_NROWS);
+    f64x2_t c3 = *reinterpret_cast<const f64x2_t*>(base + 48 * BM_RADP_NROWS);
     if (tail) {
-        // explicit loads: as plain C++ the compiler merges them with the main-table loads above into one load through
-        // a selected pointer (flat, 64-bit addresses on every lane of every radius)
-        const uint32_t rw = (uint32_t)((int)(xh >> 15) - ((1023 - 1) << 5) + (int)side * (BM_RADT_NROWS / 2)) * 16u;
+        // x = v + 1/2 itself in the tail table.  The volatile asm keeps this arithmetic inside the branch (the
+        // compiler would otherwise hoist it onto every lane), and the loads are explicit: as plain C++ they would
+        // be merged with the main-table loads above into one load through a selected pointer.
+        uint32_t vv = v;                                                // (v again, not y: y's registers are reused)
+        asm volatile("" : "+v"(vv));
+        const double x = (double)vv + 0.5;
+        const uint64_t bx = d2bits(x);
+        const uint32_t xh = (uint32_t)(bx >> 32);
+        const uint32_t rw = (uint32_t)((int)(xh >> 15) - ((1023 - 1) << 5)) * 16u + (sm & (16u * (BM_RADT_NROWS / 2)));
+        t = bits2d(((uint64_t)((xh & 0x7fffu) | 0x3ff00000u) << 32) | (bx & 0xffffffffull)) - (1.0 + 1.0 / 64.0);
         asm volatile(
-            "global_load_dwordx4 %0, %4, %8\n\t"
-            "global_load_dwordx4 %1, %5, %8\n\t"
-            "global_load_dwordx4 %2, %6, %8\n\t"
-            "global_load_dwordx4 %3, %7, %9\n\t"
+            "global_load_dwordx4 %0, %4, %5\n\t"
+            "global_load_dwordx4 %1, %4, %6\n\t"
+            "global_load_dwordx4 %2, %4, %7\n\t"
+            "global_load_dwordx4 %3, %4, %8\n\t"
             "s_waitcnt vmcnt(0)"
-            : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(cf)
-            : "v"(rw), "v"(rw + 16u * BM_RADT_NROWS), "v"(rw + 32u * BM_RADT_NROWS), "v"(rw), "s"(&kBmRadTdTab[0][0]),
-              "s"(&kBmRadTfTab[0][0])
+            : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+            : "v"(rw), "s"(&kBmRadTTab[0][0]), "s"(&kBmRadTTab[BM_RADT_NROWS][0]),
+              "s"(&kBmRadTTab[2 * BM_RADT_NROWS][0]), "s"(&kBmRadTTab[3 * BM_RADT_NROWS][0])
             : "memory");
     }
-    double q = __builtin_fma((double)cf.z, t, (double)cf.y);
-    q = __builtin_fma(q, t, (double)cf.x);
+    double q = __builtin_fma(c3.y, t, c3.x);
     q = __builtin_fma(q, t, c2.y);
     q = __builtin_fma(q, t, c2.x);
     q = __builtin_fma(q, t, c1.y);
     q = __builtin_fma(q, t, c1.x);
     q = __builtin_fma(q, t, c0.y);
-    double r = q + c0.x;
+    double r = __builtin_fma(q, t, c0.x);
     asm volatile("" : "+v"(r));     // computed here: not sunk past the next radius's branch with its coefficients live
     return r;
 }
@@ -466,23 +479,30 @@ __device__ __forceinline__ double det_log_tab(double v, const double (*tab)[4] =
 // sin, cos of 2 pi w 2^-32 (the Box-Muller angle), table-driven: the angle splits as k/1024 + j 2^-32 turns
 // with k = (w + 2^21) >> 22 and |j| <= 2^21, so r = 2 pi j 2^-32 has |r| <= 2 pi 2^-11.  The row of k gives
 // (sin a, cos a) (scripts/gen_bm_log_table.py, full circle: no quadrant selects); sin r = r - r^3/6 + r^5/120
-// (truncation r^7/5040 < 2^-70) and cos r - 1 = -r^2/2 + r^4/24 (truncation r^6/720 < 2^-59);
-// sin(a+r) = sa + (ca sin r + sa (cos r - 1)).  Round 2: 1024 rows in place of 256 (one fma fewer in each series).
+// (truncation r^7/5040 < 2^-70) and cos r = 1 - r^2/2 + r^4/24 (truncation r^6/720 < 2^-59), in j;
+// sin(a+r) = sa cos r + ca sin r, cos(a+r) = ca cos r - sa sin r, one fma each (within 2.3e-16 absolute: cos r
+// rounded to a double).  Round 2: 1024 rows in place of 256; round 3: polynomials in j, 15 VALU operations.
 static __device__ const double kBmSinCos1024Tab[1024][2] = {BM_SINCOS1024_TABLE_ROWS};
+
+// sin / cos of r = 2 pi j 2^-32 as polynomials in the integer j (round 3; RN of 2 pi 2^-32 times 1, -1/6, 1/120 and
+// of its square times -1/2, 1/24, mpmath)
+constexpr double kSinJ1 = 0x1.921fb54442d18p-30, kSinJ3 = -0x1.4abbce625be53p-91, kSinJ5 = 0x1.466bc6775aae2p-154;
+constexpr double kCosJ2 = -0x1.3bd3cc9be45dep-60, kCosJ4 = 0x1.03c1f081b5ac4p-122;
 
 __device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, double& c_out,
                                                   const double (*sct)[2] = kBmSinCos1024Tab) {
     const uint32_t k = (w + 0x200000u) >> 22;
-    // j = the sign-extended low 22 bits of w (w - 2^22 k), one v_bfe_i32
-    const double r = (double)(((int32_t)(w << 10)) >> 10) * 0x1.921fb54442d18p-30;
-    const double r2 = r * r;
-    const double sp = __builtin_fma(r2, 0x1.1111111111111p-7, -0x1.5555555555555p-3);   // 1/120, -1/6
-    const double sr = __builtin_fma(r * r2, sp, r);
-    const double cm1 = r2 * __builtin_fma(r2, 0x1.5555555555555p-5, -0.5);                // 1/24, -1/2
+    // j = the sign-extended low 22 bits of w (w - 2^22 k), one v_bfe_i32, exact in a double, and so is j^2; the
+    // polynomials are in j with 2 pi 2^-32 folded into their coefficients: sin r = j (A1 + j^2 (A3 + j^2 A5)),
+    // cos r = 1 + j^2 (B2 + j^2 B4), r = 2 pi j 2^-32, |r| <= 2 pi 2^-11
+    const double j = (double)(((int32_t)(w << 10)) >> 10);
+    const double j2 = j * j;
+    const double sr = j * __builtin_fma(j2, __builtin_fma(j2, kSinJ5, kSinJ3), kSinJ1);
+    const double cr = __builtin_fma(j2, __builtin_fma(j2, kCosJ4, kCosJ2), 1.0);
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
     const f64x2_t a = *reinterpret_cast<const f64x2_t*>(sct[k]);                   // (sin a, cos a)
-    s_out = a.x + __builtin_fma(a.y, sr, a.x * cm1);
-    c_out = a.y + __builtin_fma(-a.x, sr, a.y * cm1);
+    s_out = __builtin_fma(a.x, cr, a.y * sr);
+    c_out = __builtin_fma(a.y, cr, -(a.x * sr));
 }
 
 // IEEE sqrt of a positive normal finite x: the hardware rsq estimate refined by the same Newton/fma

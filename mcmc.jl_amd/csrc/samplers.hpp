@@ -41,15 +41,13 @@ enum TabMode : int { kTabLds = 0, kTabGlobal = 1 };
 
 struct BmLds {
     double (*rd)[2];
-    float (*rf)[4];
     double (*sc)[2];
 };
 // The block's LDS copies (one allocation per kernel, whoever asks)
 __device__ __forceinline__ BmLds bm_lds_tables() {
-    __shared__ __attribute__((aligned(16))) double lds_radd[3 * BM_RADP_NROWS][2];
-    __shared__ __attribute__((aligned(16))) float lds_radf[BM_RADP_NROWS][4];
+    __shared__ __attribute__((aligned(16))) double lds_radd[4 * BM_RADP_NROWS][2];
     __shared__ __attribute__((aligned(16))) double lds_sct[1024][2];
-    return BmLds{lds_radd, lds_radf, lds_sct};
+    return BmLds{lds_radd, lds_sct};
 }
 
 // The tables into a block's LDS by its NT threads: every 16-byte load of a batch in flight before its first store
@@ -57,15 +55,13 @@ __device__ __forceinline__ BmLds bm_lds_tables() {
 template <int NT>
 __device__ __forceinline__ void stage_bm_tables(const BmLds& L) {
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    constexpr int kD = 3 * BM_RADP_NROWS, kF = BM_RADP_NROWS, kS = 1024;     // 16-byte units of each table
-    constexpr int kU = kD + kF + kS;
+    constexpr int kD = 4 * BM_RADP_NROWS, kS = 1024;     // 16-byte units of each table
+    constexpr int kU = kD + kS;
     constexpr int kN = (kU + NT - 1) / NT;
     constexpr int kBatch = 8;
-    const f64x2_t* gd = reinterpret_cast<const f64x2_t*>(&kBmRadPdTab[0][0]);
-    const f64x2_t* gf = reinterpret_cast<const f64x2_t*>(&kBmRadPfTab[0][0]);
+    const f64x2_t* gd = reinterpret_cast<const f64x2_t*>(&kBmRadPTab[0][0]);
     const f64x2_t* gs = reinterpret_cast<const f64x2_t*>(&kBmSinCos1024Tab[0][0]);
     f64x2_t* ld = reinterpret_cast<f64x2_t*>(&L.rd[0][0]);
-    f64x2_t* lf = reinterpret_cast<f64x2_t*>(&L.rf[0][0]);
     f64x2_t* ls = reinterpret_cast<f64x2_t*>(&L.sc[0][0]);
 #pragma unroll
     for (int j0 = 0; j0 < kN; j0 += kBatch) {
@@ -73,14 +69,13 @@ __device__ __forceinline__ void stage_bm_tables(const BmLds& L) {
 #pragma unroll
         for (int j = j0; j < j0 + kBatch && j < kN; ++j) {
             const int u = (int)threadIdx.x + NT * j;
-            if (u < kU) v[j - j0] = u < kD ? gd[u] : (u < kD + kF ? gf[u - kD] : gs[u - kD - kF]);
+            if (u < kU) v[j - j0] = u < kD ? gd[u] : gs[u - kD];
         }
 #pragma unroll
         for (int j = j0; j < j0 + kBatch && j < kN; ++j) {
             const int u = (int)threadIdx.x + NT * j;
             if (u < kD) ld[u] = v[j - j0];
-            else if (u < kD + kF) lf[u - kD] = v[j - j0];
-            else if (u < kU) ls[u - kD - kF] = v[j - j0];
+            else if (u < kU) ls[u - kD] = v[j - j0];
         }
     }
     __syncthreads();
@@ -95,7 +90,7 @@ struct BmTables {
     __device__ __forceinline__ void init() {
         if constexpr (TAB == kTabLds) {
             lds = bm_lds_tables();
-            rad = RadTab{lds.rd, lds.rf};
+            rad = RadTab{lds.rd, true};
             sct = lds.sc;
         } else {
             rad = rad_tab_global();

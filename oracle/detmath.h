@@ -281,65 +281,66 @@ static inline double orc_log_tab(double v) {
 /* ------------------------------------------------------- Box-Muller angle */
 /* sin, cos of 2 pi w 2^-32: angle = k/1024 + j 2^-32 turns, k = (w + 2^21) >> 22, |j| <= 2^21; the row of k
    holds RN(sin, cos of 2 pi k/1024) (scripts/gen_bm_log_table.py, BM_SINCOS1024_TABLE_ROWS); r = 2 pi j 2^-32
-   (|r| <= 2 pi 2^-11), sin r to r^5 and cos r - 1 to r^4 (truncation < 2^-59), then the angle-addition
-   formula.  The device twin is det_sincos2pi_u32 (csrc/detmath.hpp). */
+   (|r| <= 2 pi 2^-11): sin r to r^5 and cos r to r^4 as polynomials in the integer j (2 pi 2^-32 folded into the
+   coefficients; j and j^2 exact), truncation < 2^-59, then the angle-addition formula sin = sa cos r + ca sin r,
+   cos = ca cos r - sa sin r, one fma each.  Within 2.3e-16 absolute.  The device twin is det_sincos2pi_u32
+   (csrc/detmath.hpp). */
 static const double orc_bm_sincos1024_tab[1024][2] = {BM_SINCOS1024_TABLE_ROWS};
 
+#define ORC_SIN_J1 0x1.921fb54442d18p-30
+#define ORC_SIN_J3 (-0x1.4abbce625be53p-91)
+#define ORC_SIN_J5 0x1.466bc6775aae2p-154
+#define ORC_COS_J2 (-0x1.3bd3cc9be45dep-60)
+#define ORC_COS_J4 0x1.03c1f081b5ac4p-122
+
 static inline void orc_sincos2pi_u32(uint32_t w, double* s_out, double* c_out) {
-    uint32_t t = w + 0x200000u;
-    uint32_t k = t >> 22;
-    double r = (double)((int32_t)(t & 0x3fffffu) - 0x200000) * 0x1.921fb54442d18p-30;
-    double r2 = r * r;
-    double sp = fma(r2, 0x1.1111111111111p-7, -0x1.5555555555555p-3);
-    double sr = fma(r * r2, sp, r);
-    double cm1 = r2 * fma(r2, 0x1.5555555555555p-5, -0.5);
+    uint32_t k = (w + 0x200000u) >> 22;
+    double j = (double)((int32_t)(w << 10) >> 10);        /* signed low 22 bits: w - 2^22 k */
+    double j2 = j * j;
+    double sr = j * fma(j2, fma(j2, ORC_SIN_J5, ORC_SIN_J3), ORC_SIN_J1);
+    double cr = fma(j2, fma(j2, ORC_COS_J4, ORC_COS_J2), 1.0);
     double sa = orc_bm_sincos1024_tab[k][0], ca = orc_bm_sincos1024_tab[k][1];
-    *s_out = sa + fma(ca, sr, sa * cm1);
-    *c_out = ca + fma(-sa, sr, ca * cm1);
+    *s_out = fma(sa, cr, ca * sr);
+    *c_out = fma(ca, cr, -(sa * sr));
 }
 
 /* ------------------------------------------------------- Box-Muller radius */
 /* sqrt(-2 log((w + 0.5) 2^-32)) as a table of polynomials (scripts/gen_bm_log_table.py, BM_RADP / BM_RADT): side =
-   w >> 31 folds u >= 1/2 onto 1 - u = (~w + 0.5) 2^-32 (the same radius law, exact), so x = v + 0.5 in [1/2, 2^31);
-   the binade e of x and the top 5 mantissa bits k pick a row -- side * 320 + (e - 21) * 32 + k of the main table
-   for e = 21..30, side * 704 + (e + 1) * 32 + k of the tail table for e = -1..20 (v < 2^21) -- and the radius is a
-   degree-7 polynomial in the exact residual t = m - (1 + (2k+1)/64), |t| <= 1/64 (the mantissa with its top 5
-   bits cleared, less 1 + 1/64); a0 is a hi + lo pair, a5..a7 floats.  Device twin: bm_radius_u32
-   (csrc/detmath.hpp); the same operations in the same order, so the two agree bit for bit. */
-static const double orc_bm_radpd_tab[3 * BM_RADP_NROWS][2] = {BM_RADPD_TABLE_ROWS};
-static const float orc_bm_radpf_tab[BM_RADP_NROWS][4] = {BM_RADPF_TABLE_ROWS};
-static const double orc_bm_radtd_tab[3 * BM_RADT_NROWS][2] = {BM_RADTD_TABLE_ROWS};
-static const float orc_bm_radtf_tab[BM_RADT_NROWS][4] = {BM_RADTF_TABLE_ROWS};
+   w >> 31 folds u >= 1/2 onto 1 - u = (~w + 0.5) 2^-32 (the same radius law, exact), so x = v + 0.5 in [1/2, 2^31).
+   v >= 2^21: the binade e (21..30) and top 5 mantissa bits k of v (x's are the same) pick row side * 320 +
+   (e - 21) * 32 + k of the main table, whose polynomials are in the exact residual t = m - (1 + (2k+1)/64) of v's
+   mantissa m (the 1/2 of x is inside them); v < 2^21: row side * 704 + (e + 1) * 32 + k of the tail table, binades
+   e = -1..20 of x itself, t from x's mantissa.  Degree 7 by Horner, all coefficients doubles.  Device twin:
+   bm_radius_u32 (csrc/detmath.hpp); the same operations in the same order, so the two agree bit for bit. */
+static const double orc_bm_radp_tab[4 * BM_RADP_NROWS][2] = {BM_RADP_TABLE_ROWS};
+static const double orc_bm_radt_tab[4 * BM_RADT_NROWS][2] = {BM_RADT_TABLE_ROWS};
 
 static inline double orc_bm_radius_u32(uint32_t w) {
     uint32_t side = w >> 31;
     uint32_t v = w ^ (0u - side);
-    double x = (double)v + 0.5;
-    uint64_t b = orc_d2bits(x);
-    uint32_t xh = (uint32_t)(b >> 32);
     const double (*d)[2];
-    const float* cf;
     int row, n;
+    double y;                                              /* v (main table) or x = v + 0.5 (tail) */
     if (v < (1u << 21)) {
-        row = (int)(xh >> 15) - ((1023 - 1) << 5) + (int)side * (BM_RADT_NROWS / 2);
-        d = orc_bm_radtd_tab; cf = orc_bm_radtf_tab[row]; n = BM_RADT_NROWS;
+        y = (double)v + 0.5;
+        row = (int)(orc_d2bits(y) >> 47) - ((1023 - 1) << 5) + (int)side * (BM_RADT_NROWS / 2);
+        d = orc_bm_radt_tab; n = BM_RADT_NROWS;
     } else {
-        row = (int)(xh >> 15) - ((1023 + 21) << 5) + (int)side * (BM_RADP_NROWS / 2);
-        d = orc_bm_radpd_tab; cf = orc_bm_radpf_tab[row]; n = BM_RADP_NROWS;
+        y = (double)v;
+        row = (int)(orc_d2bits(y) >> 47) - ((1023 + 21) << 5) + (int)side * (BM_RADP_NROWS / 2);
+        d = orc_bm_radp_tab; n = BM_RADP_NROWS;
     }
-    double t = orc_bits2d(((uint64_t)((xh & 0x7fffu) | 0x3ff00000u) << 32) | (b & 0xffffffffull)) -
+    uint64_t b = orc_d2bits(y);
+    uint32_t yh = (uint32_t)(b >> 32);
+    double t = orc_bits2d(((uint64_t)((yh & 0x7fffu) | 0x3ff00000u) << 32) | (b & 0xffffffffull)) -
                (1.0 + 1.0 / 64.0);
-    const double* c0 = d[row];
-    const double* c1 = d[n + row];
-    const double* c2 = d[2 * n + row];
-    double q = fma((double)cf[2], t, (double)cf[1]);
-    q = fma(q, t, (double)cf[0]);
-    q = fma(q, t, c2[1]);
-    q = fma(q, t, c2[0]);
-    q = fma(q, t, c1[1]);
-    q = fma(q, t, c1[0]);
-    q = fma(q, t, c0[1]);
-    return q + c0[0];
+    double q = fma(d[3 * n + row][1], t, d[3 * n + row][0]);  /* a7 t + a6 */
+    q = fma(q, t, d[2 * n + row][1]);
+    q = fma(q, t, d[2 * n + row][0]);
+    q = fma(q, t, d[n + row][1]);
+    q = fma(q, t, d[n + row][0]);
+    q = fma(q, t, d[row][1]);
+    return fma(q, t, d[row][0]);
 }
 
 /* Four standard normals from one Philox block (two Box-Muller pairs). */
