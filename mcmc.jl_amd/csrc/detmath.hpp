@@ -26,6 +26,10 @@ enum : uint32_t { TAG_NORMAL = 0u, TAG_ACCEPT = 1u, TAG_DATA = 7u };
 
 struct u32x4 { uint32_t x, y, z, w; };
 
+// U: c1 and c3 are wave-uniform (a step index and a tag): round 0's c1 ^ k0 and c3 ^ k1 are then scalar xors and
+// its two three-input xors single v_xor_b32 (v_bitop3_b32 reads at most one scalar operand, so with two it needs
+// a v_mov first)
+template <bool U = false>
 __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -33,10 +37,16 @@ __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
-        // three-input xor in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler's own
-        // combine leaves most of these as two v_xor_b32
-        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
-        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+        uint32_t n0, n2;
+        if (U && r == 0) {
+            n0 = (uint32_t)(p1 >> 32) ^ (c1 ^ k0);
+            n2 = (uint32_t)(p0 >> 32) ^ (c3 ^ k1);
+        } else {
+            // three-input xor in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler's own
+            // combine leaves most of these as two v_xor_b32
+            n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+            n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+        }
         c1 = (uint32_t)p1;
         c3 = (uint32_t)p0;
         c0 = n0;
@@ -50,14 +60,21 @@ struct Stream {
     __device__ __forceinline__ u32x4 block(uint32_t chain, uint32_t step, uint32_t blk, uint32_t tag) const {
         return philox4x32_10(chain, step, blk, tag, k0, k1);
     }
+    // step wave-uniform
+    __device__ __forceinline__ u32x4 block_us(uint32_t chain, uint32_t step, uint32_t blk, uint32_t tag) const {
+        return philox4x32_10<true>(chain, step, blk, tag, k0, k1);
+    }
 };
 
 __device__ __forceinline__ double bits2d(uint64_t b) { return __longlong_as_double((long long)b); }
 __device__ __forceinline__ uint64_t d2bits(double d) { return (uint64_t)__double_as_longlong(d); }
 
-__device__ __forceinline__ double uniform53(uint32_t a, uint32_t b) {
-    const uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
-    return (double)m * 0x1p-53;
+// 52-bit uniform on [0, 1) (Julia rand() semantics: 0 possible, 1 not): a:b's top 52 bits as the mantissa of a
+// double in [1, 2) -- two v_alignbit_b32 -- less 1 (round 3; was (a>>5 : b>>6) 2^-53, nine instructions)
+__device__ __forceinline__ double uniform52(uint32_t a, uint32_t b) {
+    const uint32_t hi = __builtin_amdgcn_alignbit(0x3ffu, a, 12);     // 0x3ff00000 | a >> 12
+    const uint32_t lo = __builtin_amdgcn_alignbit(a, b, 12);          // a << 20 | b >> 12
+    return bits2d(((uint64_t)hi << 32) | lo) - 1.0;
 }
 __device__ __forceinline__ double uniform32_open(uint32_t a) { return ((double)a + 0.5) * 0x1p-32; }
 __device__ __forceinline__ double uniform32(uint32_t a) { return (double)a * 0x1p-32; }
@@ -491,16 +508,18 @@ constexpr double kCosJ2 = -0x1.3bd3cc9be45dep-60, kCosJ4 = 0x1.03c1f081b5ac4p-12
 
 __device__ __forceinline__ void det_sincos2pi_u32(uint32_t w, double& s_out, double& c_out,
                                                   const double (*sct)[2] = kBmSinCos1024Tab) {
-    const uint32_t k = (w + 0x200000u) >> 22;
     // j = the sign-extended low 22 bits of w (w - 2^22 k), one v_bfe_i32, exact in a double, and so is j^2; the
     // polynomials are in j with 2 pi 2^-32 folded into their coefficients: sin r = j (A1 + j^2 (A3 + j^2 A5)),
-    // cos r = 1 + j^2 (B2 + j^2 B4), r = 2 pi j 2^-32, |r| <= 2 pi 2^-11
-    const double j = (double)(((int32_t)(w << 10)) >> 10);
+    // cos r = 1 + j^2 (B2 + j^2 B4), r = 2 pi j 2^-32, |r| <= 2 pi 2^-11.  The row's byte offset 16 k is
+    // (w - j) >> 18 (w - j = 2^22 k mod 2^32), two instructions from j.
+    const int32_t ji = ((int32_t)(w << 10)) >> 10;
+    const uint32_t off = (w - (uint32_t)ji) >> 18;                     // 16 k
+    const double j = (double)ji;
     const double j2 = j * j;
     const double sr = j * __builtin_fma(j2, __builtin_fma(j2, kSinJ5, kSinJ3), kSinJ1);
     const double cr = __builtin_fma(j2, __builtin_fma(j2, kCosJ4, kCosJ2), 1.0);
     typedef double f64x2_t __attribute__((ext_vector_type(2)));
-    const f64x2_t a = *reinterpret_cast<const f64x2_t*>(sct[k]);                   // (sin a, cos a)
+    const f64x2_t a = *reinterpret_cast<const f64x2_t*>(reinterpret_cast<const char*>(sct) + off);   // (sin a, cos a)
     s_out = __builtin_fma(a.x, cr, a.y * sr);
     c_out = __builtin_fma(a.y, cr, -(a.x * sr));
 }

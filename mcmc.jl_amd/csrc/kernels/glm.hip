@@ -637,7 +637,7 @@ __device__ __forceinline__ bool glm_mh_short_circuit(const Stream& rs, uint32_t 
     bool acc = ratio > 0.0;                                           // RWM.jl:63, MALA.jl:108
     if (!acc) {
         const u32x4 w = rs.block(chain, step, 0u, TAG_ACCEPT);
-        acc = gt_det_log(ratio, uniform53(w.x, w.y));
+        acc = gt_det_log(ratio, uniform52(w.x, w.y));
     }
     return acc;
 }
@@ -1485,7 +1485,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
             if (glm_valid(a, p, slot)) mm = __builtin_fma(m[slot], m[slot], mm);
         const double H = -lpl + 0.5 * glm_sum(a, p, L, mm);
         const u32x4 w = rs.block(chain, (uint32_t)i, 0u, TAG_ACCEPT);
-        const double u = uniform53(w.x, w.y);
+        const double u = uniform52(w.x, w.y);
         double pa = 0.0;
         bool acc;
         if (DA) {

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_la(KernelArgs a) {
 #pragma unroll
             for (int k = 0; k < NC; ++k) dz_l[buf][g][k] = z[k] * sc[k];               // randn(d) .* scale
             const u32x4 u = rs.block(chain, i, 0u, TAG_ACCEPT);
-            lu_l[buf][g] = det_log(uniform53(u.x, u.y));                               // log(rand())
+            lu_l[buf][g] = det_log(uniform52(u.x, u.y));                               // log(rand())
         }
     };
     double x[NC];
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_spec(KernelArgs a) {
 #pragma unroll
             for (int k = 0; k < D; ++k) dz_l[buf][g][k] = z[k] * sc[k];                // randn(d) .* scale
             const u32x4 u = rs.block(s.chain0, i, 0u, TAG_ACCEPT);
-            lu_l[buf][g] = det_log(uniform53(u.x, u.y));                               // log(rand())
+            lu_l[buf][g] = det_log(uniform52(u.x, u.y));                               // log(rand())
         }
     };
     auto flush = [&](int buf, int t, int nt) {       // threads t, t+nt, ... copy half buf's kept rows out

@@ -91,7 +91,7 @@ __global__ void k_seqmc_resample(int64_t N, int d, const double* cp, const int32
     int64_t src = n;
     if (*flag) {
         const u32x4 w = philox4x32_10((uint32_t)n, step, target, TAG_RESAMPLE, key0, key1);
-        const double u = uniform53(w.x, w.y);
+        const double u = uniform52(w.x, w.y);
         int64_t lo = 0, hi = N - 1;                  // cp[N-1] == 1 > u: the search always succeeds
         while (lo < hi) {
             const int64_t mid = lo + (hi - lo) / 2;

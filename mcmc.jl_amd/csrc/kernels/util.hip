@@ -79,7 +79,7 @@ __global__ void k_detmath(int op, int64_t n, const double* x, const double* y, d
         }
         case 7: r = round_away(a); break;
         case 8: { const u32x4 w = philox4x32_10((uint32_t)(uint64_t)a, 0u, 0u, TAG_ACCEPT, 0u, 0u);
-                  r = uniform53(w.x, w.y); } break;
+                  r = uniform52(w.x, w.y); } break;
         case 9: r = bm_log_u32((uint32_t)(uint64_t)a); break;
         case 10: { double s, c; det_sincos2pi_u32((uint32_t)(uint64_t)a, s, c); r = s; } break;
         case 11: { double s, c; det_sincos2pi_u32((uint32_t)(uint64_t)a, s, c); r = c; } break;

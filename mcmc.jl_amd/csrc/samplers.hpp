@@ -286,14 +286,16 @@ struct PairChain {
     __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
                                                double* base) const {
         if (base == nullptr || !live) return;
-        double* p = base + (size_t)kk * (size_t)d * (size_t)s.C;
+        // row (h NC + k) of sample kk: a wave-uniform row base (scalar registers) plus the lane's 32-bit byte offset
+        // (chain and half; a sample is d C doubles, far below 4 GiB), so each store is a saddr global_store with
+        // no per-lane 64-bit address arithmetic
         const uint64_t C = (uint64_t)s.C;
-        uint64_t o = (uint64_t)c + (uint64_t)(h * NC) * C;
+        const uint32_t lo = (uint32_t)((uint64_t)c * 8u + (uint64_t)(h * NC) * C * 8u);
+        char* row = reinterpret_cast<char*>(base + (size_t)kk * (size_t)d * (size_t)C);
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-            if (valid(k)) p[o] = v[k];
-            o += C;
-            asm volatile("" : "+v"(o));
+            if (valid(k)) *reinterpret_cast<double*>(row + lo) = v[k];
+            row += C * 8u;
         }
     }
     __device__ __forceinline__ void store_cm(const StepArgs& s, int64_t l, const double (&v)[NC], double* base) const {
@@ -441,7 +443,7 @@ __device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32
                                             double (&z)[P::NC]) {
 #pragma unroll
     for (int b = 0; b < P::NB; ++b) {
-        const u32x4 w = rs.block(chain, step, p.block(b), TAG_NORMAL);
+        const u32x4 w = rs.block_us(chain, step, p.block(b), TAG_NORMAL);
         normals4(w, z[4 * b], z[4 * b + 1], z[4 * b + 2], z[4 * b + 3], p.bt.rad, p.bt.sct);
     }
 }
@@ -486,7 +488,7 @@ __device__ __forceinline__ bool mh_accept_short_circuit(const Stream& rs, uint32
     bool acc = ratio > 0.0;
     if (!acc) {
         const u32x4 w = rs.block(chain, step, 0u, TAG_ACCEPT);
-        acc = gt_det_log(ratio, uniform53(w.x, w.y));
+        acc = gt_det_log(ratio, uniform52(w.x, w.y));
     }
     return acc;
 }
@@ -503,7 +505,7 @@ struct AcceptDraw {
             double u;
             if ((t & 1) == 0) {
                 const u32x4 w = rs.block(chain, (uint32_t)(i + p.h), 0u, TAG_ACCEPT);
-                const double uu = uniform53(w.x, w.y);
+                const double uu = uniform52(w.x, w.y);
                 u = p.from_half(uu, 0);
                 u_next = uu;
             } else {
@@ -524,6 +526,38 @@ __device__ __forceinline__ double tune_factor(int32_t acc, int32_t prop, double 
     return 1.0 / (1.0 + det_exp(-11.0 * (rate - target))) + 0.5;
 }
 
+// The kept steps of a launch (kept_index's set: local index burnin + 1 + m thinning, <= len) as a scalar
+// cursor: one 64-bit scalar compare a step instead of kept_index's 64-bit remainder and signed compares, which
+// the step loop ran on the VALU (a uniform 64-bit division and i64 compares have no scalar instructions).
+struct Keeper {
+    int64_t next;       // the next kept step (absolute index); -1: none left in this launch
+    int64_t kk;         // its kept index
+    int64_t thin;
+    int32_t left;       // kept steps after next
+    __device__ explicit Keeper(const StepArgs& s) {
+        thin = s.thinning;
+        const int64_t lo = s.step_begin - s.run_step0;                 // local index of the launch's first step
+        const int64_t hi = lo + s.nsteps - 1;
+        int64_t first = s.burnin + 1;
+        if (lo > first) first += ((lo - first + thin - 1) / thin) * thin;
+        const int64_t last = hi < s.len ? hi : s.len;
+        if (first > last) {
+            next = -1; kk = 0; left = 0;
+        } else {
+            next = s.run_step0 + first;
+            kk = (first - s.burnin - 1) / thin;
+            left = (int32_t)((last - first) / thin);
+        }
+    }
+    // kept_index(i - run_step0, ...) for the launch's steps in order
+    __device__ __forceinline__ bool take(int64_t i, int64_t* out) {
+        if (i != next) return false;
+        *out = kk;
+        if (left > 0) { next += thin; kk += 1; left -= 1; } else next = -1;
+        return true;
+    }
+};
+
 // ------------------------------------------------------------------ RWM
 // US: every coordinate has the same scale (s.scale1), held in one SGPR pair instead of d of them
 template <class P, class M, bool US = false>
@@ -541,6 +575,7 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
     AcceptDraw<P> ad;
 
+    Keeper keep(s);
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         double xp[P::NC];
@@ -557,7 +592,7 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
             lp = lpp;
         }
         int64_t kk;
-        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+        if (keep.take(i, &kk)) {
             p.store_kept(s, kk, x, s.samples);
             p.store_bit(s, kk, acc);
         }
@@ -584,6 +619,7 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
     int32_t n_prop = sa.tuner ? p.load_t(a.st.t_prop) : 0;
     AcceptDraw<P> ad;
 
+    Keeper keep(s);
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         if (sa.tuner) n_prop += 1;
@@ -621,7 +657,7 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
             if (sa.tuner) n_acc += 1;
         }
         int64_t kk;
-        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+        if (keep.take(i, &kk)) {
             p.store_kept(s, kk, x, s.samples);
             if (s.grads != nullptr) {
                 double g[P::NC];
@@ -742,6 +778,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
     const double mu = DA ? det_log(10.0) : 0.0;                 // log(10*leapStep0), leapStep0 = 1
 
     int64_t n_evals = 0;
+    Keeper keep(s);
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         if (tuned) n_prop += 1;
@@ -777,7 +814,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
         }
         const double H = -lpl + half_dot(p, m);
         const u32x4 w = rs.block(chain, (uint32_t)i, 0u, TAG_ACCEPT);
-        const double u = uniform53(w.x, w.y);
+        const double u = uniform52(w.x, w.y);
         bool acc;
         double pa = 0.0;
         if (DA) {
@@ -793,7 +830,7 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             if (tuned) n_acc += 1;
         }
         int64_t kk;
-        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+        if (keep.take(i, &kk)) {
             p.store_kept(s, kk, x0, s.samples);
             if (s.grads != nullptr) {
                 double g[P::NC];
@@ -933,6 +970,7 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
         }
         ram_matvec<NC>(ram_tile_rsrc<NC>(ram_half<NC>(T0, i - 1, ld)), vo, z, u);
     }
+    Keeper keep(s);
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         double lpp;
@@ -952,7 +990,7 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
             lp = lpp;
         }
         int64_t kk;
-        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+        if (keep.take(i, &kk)) {
             p.store_kept(s, kk, x, s.samples);
             p.store_bit(s, kk, acc);
         }
@@ -1020,6 +1058,7 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
         nz = p.reduce(a2);
         ram_wave_matvec<G>(ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld), vo, lane, d, z, u);
     }
+    Keeper keep(s);
     for (int t = 0; t < s.nsteps; ++t) {
         const int64_t i = s.step_begin + t;
         double lpp;
@@ -1038,7 +1077,7 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
             lp = lpp;
         }
         int64_t kk;
-        if (kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk)) {
+        if (keep.take(i, &kk)) {
             p.store_kept(s, kk, x, s.samples);
             p.store_bit(s, kk, acc);
         }

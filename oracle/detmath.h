@@ -11,7 +11,7 @@
  *
  *   Philox4x32-10 ..... Salmon et al., SC'11 (Random123); pinned by the
  *                       Random123 known-answer vectors (tests/golden/philox_kat.json)
- *   uniform53 ......... 53-bit uniform on [0,1)  (Julia `rand()` semantics: 0 possible, 1 not)
+ *   uniform52 ......... 52-bit uniform on [0,1)  (Julia `rand()` semantics: 0 possible, 1 not)
  *   det_log ........... fdlibm e_log.c algorithm (Sun, 1993), branch-free general
  *                       path, explicit fma in the polynomial
  *   det_exp ........... Cody-Waite reduction + degree-13 Taylor (fma Horner)
@@ -69,10 +69,11 @@ static inline void orc_block(uint64_t seed, uint32_t chain, uint32_t step, uint3
 static inline double orc_bits2d(uint64_t b) { double d; memcpy(&d, &b, 8); return d; }
 static inline uint64_t orc_d2bits(double d) { uint64_t b; memcpy(&b, &d, 8); return b; }
 
-/* 53-bit uniform on [0,1) from two 32-bit words. */
-static inline double orc_uniform53(uint32_t a, uint32_t b) {
-    uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
-    return (double)m * 0x1p-53;
+/* 52-bit uniform on [0,1) from two 32-bit words: the top 52 bits of a:b as the mantissa of a double in [1, 2),
+   less 1 (device twin: uniform52). */
+static inline double orc_uniform52(uint32_t a, uint32_t b) {
+    uint64_t bits = ((uint64_t)(0x3ff00000u | (a >> 12)) << 32) | (uint64_t)((a << 20) | (b >> 12));
+    return orc_bits2d(bits) - 1.0;
 }
 /* 32-bit uniform on (0,1): never 0, never 1. */
 static inline double orc_uniform32_open(uint32_t a) { return ((double)a + 0.5) * 0x1p-32; }

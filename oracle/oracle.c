@@ -427,7 +427,7 @@ static void orc_normals(uint64_t seed, uint32_t chain, uint32_t step, int d, dou
 static double orc_accept_uniform(uint64_t seed, uint32_t chain, uint32_t step) {
     uint32_t w[4];
     orc_block(seed, chain, step, 0u, ORC_TAG_ACCEPT, w);
-    return orc_uniform53(w[0], w[1]);
+    return orc_uniform52(w[0], w[1]);
 }
 
 /* i in r = (burnin+1):thinning:len ?  (SerialMC.jl:35, :49) */
@@ -837,7 +837,7 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
                 uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
                 uint32_t key[2] = {0u, 0u}, w[4];
                 orc_philox4x32_10(ctr, key, w);
-                r = orc_uniform53(w[0], w[1]);
+                r = orc_uniform52(w[0], w[1]);
             } break;
             default: r = 0.0;
         }
@@ -1014,7 +1014,7 @@ void orc_seqmc(const orc_model* const* models, const orc_sampler* const* sampler
                 for (int64_t n = 0; n < N; ++n) {
                     uint32_t w[4];
                     orc_block(seed, (uint32_t)n, (uint32_t)i, (uint32_t)t, ORC_TAG_RESAMPLE, w);
-                    const double u = orc_uniform53(w[0], w[1]);
+                    const double u = orc_uniform52(w[0], w[1]);
                     int64_t lo = 0, hi = N - 1;
                     while (lo < hi) {
                         int64_t mid = lo + (hi - lo) / 2;

@@ -42,10 +42,15 @@ def randn(seed, chain, step, d):
     return np.array(z[:d])
 
 
+def _u52(a, b):
+    """The build's rand(): the top 52 bits of a:b as a fraction (exact in a double)."""
+    return float(((a << 20) | (b >> 12)) & ((1 << 52) - 1)) * 2.0**-52
+
+
 def rand(seed, chain, step):
-    """rand(): a 53-bit uniform from block (chain, step, 0, ACCEPT=1)."""
+    """rand(): a 52-bit uniform from block (chain, step, 0, ACCEPT=1)."""
     w = _block(seed, chain, step, 0, 1)
-    return float(((w[0] >> 5) << 26) | (w[1] >> 6)) * 2.0**-53
+    return _u52(int(w[0]), int(w[1]))
 
 
 def jexp(x):
@@ -496,7 +501,7 @@ def literal_seqmc(targets, particles, steps, burnin, trigger, seed):
                 rs = [0] * npart
                 for n in range(npart):
                     w = _block(seed, n, i, t, 2)
-                    l = float(((w[0] >> 5) << 26) | (w[1] >> 6)) * 2.0**-53
+                    l = _u52(int(w[0]), int(w[1]))
                     rs[n] = int(np.argmax(cp >= l))               # findfirst(p -> p >= l, cp)
                 pars = [pars[r].copy() for r in rs]
                 logW = np.zeros(npart)

@@ -144,7 +144,7 @@ def test_normals_are_standard_normal():
     assert np.abs(z).max() < 6.77
 
 
-def test_uniform53_range():
+def test_uniform52_range():
     u = orc.detmath(8, np.arange(20000, dtype=float))
     assert u.min() >= 0.0 and u.max() < 1.0
     assert stats.kstest(u, "uniform").pvalue > 1e-3
