@@ -191,6 +191,40 @@ def measured_valu(kname, wkey):
     return None
 
 
+def glm_src_hash():
+    """sha256 over the sources the regression step kernels are compiled from (csrc/*.hpp, the tables,
+    kernels/glm*.hip): an fp64 profile recorded under another hash measured other code."""
+    import glob
+    import hashlib
+    base = os.path.join(ROOT, "mcmc.jl_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(base, "*.hpp")) + glob.glob(os.path.join(base, "*.inc"))
+                   + glob.glob(os.path.join(base, "kernels", "glm*.hip")))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, base).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def measured_fp64(kname, wkey):
+    """The regression kernel's fp64 work per evaluation (MFMA flops and VALU fp64 flops) from a committed
+    rocprofv3 PMC run of this kernel instance, these sources and this workload (profiles/fp64.json, written by
+    scripts/summarize_fp64.py), or None.  fp64 MFMA and fp64 VALU share one datapath on CDNA4,
+    so the combined rate is the bound the line reports beside the MFMA-only fraction."""
+    p = os.path.join(ROOT, "profiles", "fp64.json")
+    if not os.path.exists(p):
+        return None
+    h = glm_src_hash()
+
+    def shape(key):                      # per-evaluation work does not depend on the step count or thinning
+        return "|".join(f for f in (key or "").split("|") if not f.startswith(("steps=", "thinning=")))
+    for k, e in json.load(open(p)).items():
+        if (_norm_kernel(e.get("kernel", k)) == _norm_kernel(kname) and e.get("src_hash") == h
+                and shape(e.get("workload_key")) == shape(wkey)):
+            return e
+    return None
+
+
 def host_cpus():
     """The host cores this process may use: its CPU affinity set, capped by the cgroup's CPU quota when one is
     set (a GPU box shows every CPU of the machine in nproc / os.cpu_count() but grants a share of them), plus
@@ -563,6 +597,17 @@ def main():
                 "evals_per_launch": evals / launches,
                 "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
                         "device); 4 n d fp64 flop each (SURVEY.md §8(d))"}
+        fm = measured_fp64(kname, wkey)
+        if fm is not None:                                            # MFMA + VALU fp64 on the shared datapath
+            per_eval = fm["mfma_flop_per_eval"] + fm["valu_fp64_flop_per_eval"]
+            comb = per_eval * evals / launches / avg_launch_s / 1e12
+            roof["fp64_combined"] = {
+                "achieved": comb, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": comb / F64_MFMA_PEAK_TFS,
+                "mfma_flop_per_eval": fm["mfma_flop_per_eval"], "valu_fp64_flop_per_eval": fm["valu_fp64_flop_per_eval"],
+                "source": fm["source"],
+                "note": "fp64 MFMA and fp64 VALU instructions share the SIMD's fp64 datapath: (measured MFMA flops + "
+                        "64 x SQ_INSTS_VALU_FLOPS_FP64 per evaluation of a committed PMC profile) x the live "
+                        "launch's evaluations / its time"}
     # acceptance over the timed run's kept steps (accept bits, SerialMC.jl:55-63)
     pop8 = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.float64, device=dev)
     acceptance = float(pop8[bits.view(torch.uint8).long()].sum()) / max(1, nkept * C)
