@@ -188,8 +188,8 @@ def test_bench_traffic_only_from_a_profile_of_the_same_kernel():
     assert bench.measured_traffic("no-such-workload", "lpc_rwm") is None
     # the driver's exact command (bench.py --gpus 1 --steps 20 --warmup 5) has a committed profile
     dkey = "metric|d=32|chains=1048576|rwm|steps=20|thinning=10|spl=0"
-    assert bench.measured_traffic(dkey, "lpc_rwm<8, true, IsoDot, true>") is not None
-    assert bench.measured_traffic(dkey, "lpc_rwm<8, true, IsoDot, false>") is None
+    assert bench.measured_traffic(dkey, "lpp_rwm<4, true, IsoDot, true>") is not None     # two lanes per chain
+    assert bench.measured_traffic(dkey, "lpp_rwm<4, true, IsoDot, false>") is None
 
 
 def test_bench_valu_roofline_profile():
