@@ -252,9 +252,13 @@ def host_cpus():
     return {"usable": usable, "nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota, "model": model}
 
 
-def cpu_baseline(model, sampler, seconds, C=4096):
+def cpu_baseline(model, sampler, seconds, C=4096, leaps_per_step=None):
     """The oracle (scalar C port of SerialMC + sampler, OpenMP over chains) on a bounded sample, on every host
-    core this process may use (host_cpus); a one-chain workload (config 1) is timed as one chain on one core."""
+    core this process may use (host_cpus); a one-chain workload (config 1) is timed as one chain on one core.
+    leaps_per_step: an adaptive-trajectory sampler (HMCDA) whose cost per step depends on the adapted step size:
+    the sample then runs without adaptation (burnin 0) and is converted from leapfrogs/s at the GPU run's
+    measured leapfrogs per chain-step -- adapting on the host first would take minutes (config 5: ~300 leapfrogs
+    of 8.4 Mflop per chain-step once adapted)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref as orc
     import mcmchip as mc
@@ -266,12 +270,21 @@ def cpu_baseline(model, sampler, seconds, C=4096):
     steps, dt = 1, 0.0
     while True:
         oc = orc.OracleChains(model, sampler, nchains=C, seed=1)
+        burnin = 0 if leaps_per_step else steps // 10
         t0 = time.perf_counter()
-        oc.run(mc.SerialMC(steps=steps, burnin=steps // 10, thinning=10 if steps >= 20 else 1), nthreads=threads)
+        oc.run(mc.SerialMC(steps=steps, burnin=burnin, thinning=10 if steps >= 20 else 1), nthreads=threads)
         dt = time.perf_counter() - t0
+        print(f"bench: cpu_baseline sample {C} chains x {steps} steps: {dt:.2f} s", file=sys.stderr, flush=True)
         if dt >= seconds / 2 or steps >= 1 << 25:
             break
         steps *= 2 if dt > seconds / 16 else 4
+    if leaps_per_step:
+        leaps = float(np.sum(oc.n_evals))
+        return {"value": leaps / dt / leaps_per_step, "unit": "chain-steps/s", "cores": threads, "kind": "port",
+                "host": host, "leapfrogs_per_s": leaps / dt, "leapfrogs_per_chain_step": leaps_per_step,
+                "sample": f"{C} chains x {steps} steps on the host without adaptation ({leaps:.0f} leapfrogs, "
+                          f"{dt:.1f} s), oracle/oracle.c OpenMP over {threads} threads; chain-steps/s = leapfrogs/s "
+                          f"/ the GPU run's {leaps_per_step:.1f} leapfrogs per adapted chain-step"}
     return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
             "host": host,
             "sample": f"{C} chains x {steps} steps of the same workload on the host ({dt:.1f} s), "
@@ -411,8 +424,10 @@ def main():
         wout = _lib.Outputs()
         cfg = wr.cfg()
         ta = time.perf_counter()
+        print(f"bench: warmup {W} steps", file=sys.stderr, flush=True)   # progress on stderr (stdout: the line)
         _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(wout)))
         torch.cuda.synchronize(dev)
+        print(f"bench: warmup done in {time.perf_counter() - ta:.1f} s", file=sys.stderr, flush=True)
         if cfg0.get("adapt"):
             eps = task.tuner_state()["step_bar"]
             adapt = {"warmup": f"SerialMC(steps={W + 1}, burnin={W}): {W - 1} dual-averaging updates, untimed",
@@ -433,6 +448,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     T = time.perf_counter() - t0
+    print(f"bench: timed {K} steps in {T:.3f} s", file=sys.stderr, flush=True)
     kernel_ms = out.kernel_ms
     evals = task.evals - ev0
     if dist is not None:
@@ -650,8 +666,9 @@ def main():
     if pcie is not None:
         line["pcie_inclusive"] = pcie
     if rank == 0 and not args.no_cpu_baseline:          # after the timed region, also on N > 1 lines
+        lps = evals / (C * K) if args.sampler == "hmcda" else None
         line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,
-                                            C=min(C, 4096 if cfg0["model"] == "iso" else 64))
+                                            C=min(C, 4096 if cfg0["model"] == "iso" else 64), leaps_per_step=lps)
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     if dist is not None:

@@ -7,9 +7,11 @@
 
 namespace mcmc {
 
-// F: d == 4 NB (LaneChain FULL); US: uniform RWM scale.  RWM (config 2, d = 3): 768-thread blocks reading the
-// Box-Muller tables from LDS (56 KB a block: two blocks, six waves per SIMD); MALA / HMC read them from global memory
-constexpr int kLpcRwmThreads = 768;
+// F: d == 4 NB (LaneChain FULL); US: uniform RWM scale.  RWM (config 2, d = 3): 512-thread blocks reading the
+// Box-Muller tables from LDS (56 KB a block: two blocks a CU, four waves per SIMD), so 2^20 chains are exactly four
+// rounds of the 512 resident blocks (768-thread blocks, six waves per SIMD, left a 2/3-full last round: CU busy
+// 0.87 of the launch, 1.47e11 against 1.63e11 chain-steps/s); MALA / HMC read the tables from global memory
+constexpr int kLpcRwmThreads = 512;
 template <int NB, bool F, class M, bool US>
 __global__ __launch_bounds__(kLpcRwmThreads) void lpc_rwm(KernelArgs a) {
     rwm_body<LaneChain<NB, F, false, kLpcRwmThreads, kTabLds>, M, US>(a);

@@ -76,6 +76,6 @@ from bench import step_kernel_src_hash  # noqa: E402
 entry["src_hash"] = step_kernel_src_hash()   # the sources this profile measured (bench.py ignores other hashes)
 p = os.path.join(root, "profiles", "valu.json")
 tj = json.load(open(p)) if os.path.exists(p) else {}
-tj[kname] = entry
+tj[f"{kname}|{entry['workload_key']}"] = entry        # one entry per kernel and workload
 json.dump(tj, open(p, "w"), indent=1, sort_keys=True)
 print("\n".join(L))
