@@ -345,7 +345,9 @@ __device__ __forceinline__ double bm_radius_u32(uint32_t w, RadTab rt) {
     if (tail) {
         // x = v + 1/2 itself in the tail table.  The volatile asm keeps this arithmetic inside the branch (the
         // compiler would otherwise hoist it onto every lane), and the loads are explicit: as plain C++ they would
-        // be merged with the main-table loads above into one load through a selected pointer.
+        // be merged with the main-table loads above into one load through a selected pointer.  (A fully unrolled
+        // region with many of these branches can still spill: the fused RAM update draws its normals before it,
+        // samplers.hpp ram_body kZLds.)
         uint32_t vv = v;                                                // (v again, not y: y's registers are reused)
         asm volatile("" : "+v"(vv));
         const double x = (double)vv + 0.5;

@@ -10,16 +10,25 @@ namespace mcmc {
 // F: d == 4 NB (LaneChain FULL); US: uniform RWM scale.  RWM (config 2, d = 3): 512-thread blocks reading the
 // Box-Muller tables from LDS (56 KB a block: two blocks a CU, four waves per SIMD), so 2^20 chains are exactly four
 // rounds of the 512 resident blocks (768-thread blocks, six waves per SIMD, left a 2/3-full last round: CU busy
-// 0.87 of the launch, 1.47e11 against 1.63e11 chain-steps/s); MALA / HMC read the tables from global memory
+// 0.87 of the launch, 1.47e11 against 1.63e11 chain-steps/s); MALA / HMC (256 threads, two waves per SIMD by their
+// registers, so two blocks a CU) read them from LDS too
 constexpr int kLpcRwmThreads = 512;
 template <int NB, bool F, class M, bool US>
 __global__ __launch_bounds__(kLpcRwmThreads) void lpc_rwm(KernelArgs a) {
     rwm_body<LaneChain<NB, F, false, kLpcRwmThreads, kTabLds>, M, US>(a);
 }
+// MALA / HMC block size: two 56 KB-LDS blocks a CU, sized so that they fill the occupancy the registers allow
+// (d <= 4: 125 VGPRs, four waves per SIMD; d <= 8: ~155, three; d <= 16: ~200-240, two)
+template <int NB>
+constexpr int lpc_grad_threads() { return NB == 1 ? 512 : (NB == 2 ? 768 : 256); }
 template <int NB, bool F, class M>
-__global__ __launch_bounds__(kBlock, 2) void lpc_mala(KernelArgs a) { mala_body<LaneChain<NB, F>, M>(a); }
+__global__ __launch_bounds__((lpc_grad_threads<NB>()), (lpc_grad_threads<NB>() / 256)) void lpc_mala(KernelArgs a) {
+    mala_body<LaneChain<NB, F, false, lpc_grad_threads<NB>(), kTabLds>, M>(a);
+}
 template <int NB, bool F, class M, bool DA>
-__global__ __launch_bounds__(kBlock) void lpc_hmc(KernelArgs a) { hmc_body<LaneChain<NB, F>, M, DA>(a); }
+__global__ __launch_bounds__((lpc_grad_threads<NB>()), (lpc_grad_threads<NB>() / 256)) void lpc_hmc(KernelArgs a) {
+    hmc_body<LaneChain<NB, F, false, lpc_grad_threads<NB>(), kTabLds>, M, DA>(a);
+}
 template <int NB, class M>
 __global__ __launch_bounds__(kBlock) void lpc_eval(KernelArgs a, const double* xin, double* lp, double* g,
                                                    int32_t check) {
@@ -368,6 +377,7 @@ static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
         else lpc_rwm_la<NB, M, false><<<1, kBlock, 0, st>>>(a);
     } else {
         const dim3 grid((unsigned)((a.s.C + kBlock - 1) / kBlock));
+        auto gridT = [&](int threads) { return dim3((unsigned)((a.s.C + threads - 1) / threads)); };
         const char* b = F ? "true" : "false";
         switch (a.sa.kind) {
             case SK_RWM:
@@ -396,15 +406,15 @@ static hipError_t lpc_launch_model(const KernelArgs& a, hipStream_t st) {
                 break;
             case SK_MALA:
                 mcmc_note_step_kernel("lpc_mala<%d, %s, %s>", NB, b, M::kName);
-                lpc_mala<NB, F, M><<<grid, kBlock, 0, st>>>(a);
+                lpc_mala<NB, F, M><<<gridT(lpc_grad_threads<NB>()), lpc_grad_threads<NB>(), 0, st>>>(a);
                 break;
             case SK_HMC:
                 mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, false>", NB, b, M::kName);
-                lpc_hmc<NB, F, M, false><<<grid, kBlock, 0, st>>>(a);
+                lpc_hmc<NB, F, M, false><<<gridT(lpc_grad_threads<NB>()), lpc_grad_threads<NB>(), 0, st>>>(a);
                 break;
             case SK_HMCDA:
                 mcmc_note_step_kernel("lpc_hmc<%d, %s, %s, true>", NB, b, M::kName);
-                lpc_hmc<NB, F, M, true><<<grid, kBlock, 0, st>>>(a);
+                lpc_hmc<NB, F, M, true><<<gridT(lpc_grad_threads<NB>()), lpc_grad_threads<NB>(), 0, st>>>(a);
                 break;
             default: return hipErrorInvalidValue;
         }
@@ -506,8 +516,12 @@ static hipError_t lpc_record_m(const KernelArgs& a, const LeapRec& r, hipStream_
 // defines mcmc_lpc_ram_iso.
 namespace mcmc {
 template <int NB, class M>
-// d > 16: the log-target in PairChain's order (LaneChain SPLIT), as the chains' model.eval (lpp_eval) forms it
-__global__ __launch_bounds__(kBlock, NB <= 4 ? 2 : 1) void lpc_ram(KernelArgs a) { ram_body<LaneChain<NB, false, (NB > 4)>, M>(a); }
+// d > 16: the log-target in PairChain's order (LaneChain SPLIT), as the chains' model.eval (lpp_eval) forms it.
+// The next step's rvec from LDS (ram_body kZLds) and the Box-Muller tables from LDS too, except at 12 < d <= 16,
+// where 56 KB of tables beside the 32 KB rvec would leave one block a CU and the registers allow two
+__global__ __launch_bounds__(kBlock, NB <= 4 ? 2 : 1) void lpc_ram(KernelArgs a) {
+    ram_body<LaneChain<NB, false, (NB > 4), kBlock, NB == 4 ? kTabGlobal : kTabLds>, M>(a);
+}
 
 template <class M>
 static hipError_t lpc_ram_step(const KernelArgs& a, hipStream_t st) {

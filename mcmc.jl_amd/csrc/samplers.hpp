@@ -957,7 +957,16 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
     double* const T0 = a.st.ram_L + (uint64_t)tile * (uint64_t)ram_tile_doubles(NC);
     const uint32_t vo = (threadIdx.x & 63) * 8;
     // rvec = randn(d) of step i and its S * rvec: the launch's first step forms them here, every later one
-    // inside the previous step's factor update (ram_update<NEXT = true>), so a step reads the factor once
+    // inside the previous step's factor update (ram_update<NEXT = true>), so a step reads the factor once.
+    // kZLds (d > 4): the next rvec is drawn before the update into the lane's LDS slots and read back inside it:
+    // the Box-Muller radius's rare-tail branches inside the fully unrolled factor sweep made it spill (800+ VGPRs at
+    // d = 32).  8 KB a Philox block beside the 56 KB tables: two 256-thread blocks a CU up to d = 12, one beyond.
+    constexpr bool kZLds = P::NB > 1;
+    double* zlds = nullptr;
+    if constexpr (kZLds) {
+        __shared__ double zbuf[4 * P::NB * kBlock];
+        zlds = zbuf;
+    }
     double u[NC], nz = 0.0;
     if (s.nsteps > 0) {
         const int64_t i = s.step_begin;
@@ -998,7 +1007,7 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
         const ram_rsrc_t Ss = ram_tile_rsrc<NC>(ram_half<NC>(T0, i - 1, ld));
         const ram_rsrc_t Sd = ram_tile_rsrc<NC>(ram_half<NC>(T0, i, ld));
         double un[NC], nzn = 0.0;
-        auto zblock = [&](int b, double (&z4)[4]) {                           // step i + 1's rvec, block b
+        auto zgen = [&](int b, double (&z4)[4]) {                             // step i + 1's rvec, block b
             const u32x4 w = rs.block(chain, (uint32_t)(i + 1), p.block(b), TAG_NORMAL);
             normals4(w, z4[0], z4[1], z4[2], z4[3], p.bt.rad, p.bt.sct);
 #pragma unroll
@@ -1007,6 +1016,23 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
                 nzn = __builtin_fma(z4[e], z4[e], nzn);
             }
         };
+        auto zblock = [&](int b, double (&z4)[4]) {
+            if constexpr (kZLds) {                                            // drawn before the update
+#pragma unroll
+                for (int e = 0; e < 4; ++e) z4[e] = zlds[(4 * b + e) * kBlock + threadIdx.x];
+            } else {
+                zgen(b, z4);
+            }
+        };
+        if (kZLds && t + 1 < s.nsteps) {
+#pragma unroll
+            for (int b = 0; b < P::NB; ++b) {
+                double z4[4];
+                zgen(b, z4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) zlds[(4 * b + e) * kBlock + threadIdx.x] = z4[e];
+            }
+        }
         if (t + 1 < s.nsteps) {
             ram_update<NC, true>(Ss, Sd, vo, alpha, nz, u, zblock, un);
 #pragma unroll
