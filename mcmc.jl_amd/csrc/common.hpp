@@ -81,6 +81,8 @@ struct StepArgs {
     int64_t nw;                 // words per kept step = ceil(C/64)
     int32_t* err;               // device error word
     unsigned long long* n_evals;  // running count of log-target evaluations over all chains (NULL: off)
+    const int32_t* order;       // regression HMC / HMCDA: chain slot -> local chain (NULL: identity), so that a
+                                // 16-chain MFMA tile holds chains of similar trajectory length
 };
 
 // storeLeaps record of one kept step (HMC.jl:145-150): device pointers already offset to that step;

@@ -103,10 +103,13 @@ struct mcmc_chains {
     int32_t scale_uniform = 0;
     double* d_init_x = nullptr;      // optional per-chain start, [d][C]
     unsigned long long* d_evals = nullptr;   // log-target evaluations since create/reset (all chains)
+    int64_t h_evals = 0;             // ... of the samplers with one evaluation per chain-step, counted here
     int64_t steps_done = 0;
     int64_t spl = 0;                 // steps per launch (0: whole run)
     int store_grads = 1;
     DevBuf out_samples, out_grads, out_bits, out_tmp, stage_samples, stage_grads;
+    DevBuf order_buf;                // regression HMC / HMCDA: chain slot -> chain (StepArgs.order)
+    std::vector<int32_t> h_order;
     // storeLeaps (HMC.jl:145-150): host buffers the next run fills (h_lpars == NULL: off), device staging
     int64_t leap_cap = 0;
     double *h_lpars = nullptr, *h_lgrads = nullptr, *h_lmom = nullptr, *h_llp = nullptr, *h_lH = nullptr;
@@ -543,6 +546,45 @@ static void free_state(mcmc_chains* c) {
     s = ChainState{};
 }
 
+// RWM, MALA and RAM evaluate the log-target once per chain-step, so a launch of n steps adds C n evaluations:
+// counted on the host.  The step kernels count only where the count is data-dependent (HMC / HMCDA trajectories):
+// one device-scope atomic per wave on a single address serialises at the memory side (32 768 of them per 2^20-chain
+// launch of the pair kernel, ~10 ns apart) and held a short launch's tail for hundreds of microseconds.
+static bool evals_on_host(const mcmc_chains* c) {
+    return c->sa.kind == SK_RWM || c->sa.kind == SK_MALA || c->sa.kind == SK_RAM;
+}
+
+// Regression HMC / HMCDA: the chains' order for the next run, longest trajectory first.  A 16-chain MFMA tile runs
+// its leapfrog loop to the longest trajectory among its chains (glm_hmc's glm_max), and an HMCDA chain's length
+// round(len / leapStep) follows its own adapted leapStep (config 5: 240 to 384 leapfrogs a step), so tiles of
+// arbitrary chains idle on ~10% of their leapfrogs; sorted, a tile's chains take (nearly) the same number, and the
+// longest tiles are dispatched first.  Bitwise neutral: a tile's MFMA columns are independent chains, and every
+// chain-indexed access goes through the permutation (glm.hip glm_pos).  The key is the state the run starts from:
+// the current leapStep (HMCDA; smaller is longer, NaN last) or the tuned nLeaps (HMC).
+static int glm_trajectory_order(mcmc_chains* c, hipStream_t st) {
+    mcmc_ctx* ctx = c->model->ctx;
+    const int64_t C = c->C;
+    if (int rc = ensure(c->order_buf, (size_t)C * sizeof(int32_t))) return rc;
+    std::vector<double> key((size_t)C);
+    if (c->sa.kind == SK_HMCDA) {
+        HIP_TRY(d2h(ctx, key.data(), c->st.t_step, (size_t)C * sizeof(double)));
+    } else {
+        std::vector<int32_t> nl((size_t)C);
+        HIP_TRY(d2h(ctx, nl.data(), c->st.t_leaps, (size_t)C * sizeof(int32_t)));
+        for (int64_t i = 0; i < C; ++i) key[(size_t)i] = -(double)nl[(size_t)i];
+    }
+    c->h_order.resize((size_t)C);
+    for (int64_t i = 0; i < C; ++i) c->h_order[(size_t)i] = (int32_t)i;
+    std::stable_sort(c->h_order.begin(), c->h_order.end(), [&](int32_t a, int32_t b) {
+        const double ka = key[(size_t)a], kb = key[(size_t)b];
+        const bool na = std::isnan(ka), nb = std::isnan(kb);
+        return na != nb ? nb : (!na && ka < kb);
+    });
+    HIP_TRY(hipMemcpyAsync(c->order_buf.p, c->h_order.data(), (size_t)C * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return MCMC_OK;
+}
+
 // Put every chain at its start and reset the sampler's state (SamplerTask initialisation).
 static int init_state(mcmc_chains* c) {
     mcmc_model* m = c->model;
@@ -552,6 +594,7 @@ static int init_state(mcmc_chains* c) {
     hipStream_t st = ctx->stream;
     HIP_TRY(hipMemsetAsync(ctx->d_err, 0, sizeof(int32_t), st));
     HIP_TRY(hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), st));
+    c->h_evals = 0;
     if (c->d_init_x) {
         HIP_TRY(cols_to_state(c->layout, c->st.x, c->ld, c->d_init_x, c->C, d, c->C, st));
     } else if (c->layout == LAYOUT_WPC) {       // chain-major [C][ld]
@@ -719,6 +762,7 @@ extern "C" int mcmc_chains_destroy(mcmc_chains* c) {
     dfree(c->d_init_x);
     dfree(c->d_evals);
     dfree(c->out_samples.p);
+    dfree(c->order_buf.p);
     dfree(c->out_grads.p);
     dfree(c->out_bits.p);
     dfree(c->out_tmp.p);
@@ -742,7 +786,7 @@ extern "C" int mcmc_chains_evals(mcmc_chains* c, int64_t* evals) {
     if (int r = set_device(ctx)) return r;
     unsigned long long v = 0;
     HIP_TRY(d2h(ctx, &v, c->d_evals, sizeof v));
-    *evals = (int64_t)v;
+    *evals = (int64_t)v + c->h_evals;
     return MCMC_OK;
 }
 
@@ -990,7 +1034,13 @@ int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs*
     s.grads = k_grads;
     s.acc_bits = d_bits;
     s.nw = nw;
-    s.n_evals = c->d_evals;
+    const bool host_evals = evals_on_host(c);
+    s.n_evals = host_evals ? nullptr : c->d_evals;
+    s.order = nullptr;
+    if (L == LAYOUT_GLM && C > 16 && (c->sa.kind == SK_HMCDA || (c->sa.kind == SK_HMC && c->sa.tuner))) {
+        if (int rc = glm_trajectory_order(c, st)) return rc;
+        s.order = (const int32_t*)c->order_buf.p;
+    }
 
     // storeLeaps: one step per launch; before each kept step, a record launch of its trajectory
     const bool rec = c->h_lpars != nullptr;
@@ -1028,6 +1078,7 @@ int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs*
         g_step_kernel[0] = 0;
         HIP_TRY(launch_step(L, a, st));
         c->step_kernel = g_step_kernel;
+        if (host_evals) c->h_evals += C * n;
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     if (L == LAYOUT_WPC) {
@@ -1119,10 +1170,11 @@ static int step_once(mcmc_chains* c, hipStream_t st) {
     s.grads = nullptr;
     s.acc_bits = nullptr;
     s.nw = (c->C + 63) / 64;
-    s.n_evals = c->d_evals;
+    s.n_evals = evals_on_host(c) ? nullptr : c->d_evals;
     s.step_begin = c->steps_done + 1;
     s.nsteps = 1;
     HIP_TRY(launch_step(c->layout, a, st));
+    if (evals_on_host(c)) c->h_evals += c->C;
     c->steps_done += 1;
     return MCMC_OK;
 }

@@ -94,8 +94,11 @@ __device__ __forceinline__ GlmPos glm_pos(const GlmArgs& a) {
     p.wave = threadIdx.x >> 6;
     p.slice = p.wave % a.g.nw;
     p.tile = p.wave / a.g.nw;
-    p.c = ((int64_t)blockIdx.x * a.g.tpw + p.tile) * 16 + p.cl;
-    p.live = p.c < a.s.C;
+    const int64_t slot = ((int64_t)blockIdx.x * a.g.tpw + p.tile) * 16 + p.cl;
+    p.live = slot < a.s.C;
+    // every chain-indexed access below goes through p.c; a tile's MFMA columns are independent chains, so the
+    // permutation changes which chains share a tile (and its leapfrog loop), never a chain's arithmetic
+    p.c = (a.s.order != nullptr && p.live) ? (int64_t)a.s.order[slot] : slot;
     p.base = p.slice * a.g.ds;
     return p;
 }
@@ -608,10 +611,20 @@ __device__ __forceinline__ void glm_count_evals(const GlmArgs& a, const GlmPos& 
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
     if (p.lane == 0) atomicAdd(a.s.n_evals, v);
 }
+// the tile's accept bits of a kept step (called by every lane of the wave): its 16 chains are consecutive from
+// c0 = 16 (block tpw + tile), i.e. bits c0 & 63 .. +15 of one word, set by one atomic per wave (a per-chain
+// atomicOr put up to 64 device-scope atomics on every word)
 __device__ __forceinline__ void glm_store_bit(const GlmArgs& a, const GlmPos& p, int64_t kk, bool acc) {
-    if (p.live && acc && p.q == 0 && p.slice == 0 && a.s.acc_bits != nullptr)
+    if (a.s.order != nullptr) {                                  // permuted tile: chains anywhere, a bit each
+        if (p.live && acc && p.q == 0 && p.slice == 0 && a.s.acc_bits != nullptr)
+            atomicOr((unsigned long long*)&a.s.acc_bits[(size_t)kk * (size_t)a.s.nw + (size_t)(p.c >> 6)],
+                     1ull << (p.c & 63));
+        return;
+    }
+    const uint64_t m = __ballot(p.live && acc && p.q == 0 && p.slice == 0) & 0xffffull;   // lane cl < 16: bit cl
+    if (p.lane == 0 && m != 0 && a.s.acc_bits != nullptr)                                   // lane 0: c == c0
         atomicOr((unsigned long long*)&a.s.acc_bits[(size_t)kk * (size_t)a.s.nw + (size_t)(p.c >> 6)],
-                 1ull << (p.c & 63));
+                 (unsigned long long)(m << (p.c & 63)));
 }
 
 // normals of the lane's coordinates; padded coordinates (k >= d) get 0 so they stay at 0
