@@ -315,6 +315,9 @@ int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr /*[n][4]*/, 
 /* nk chained v_mfma_f64_16x16x4_f64: D = A[16][4nk] * B[4nk][16] + C[16][16] (row-major, host pointers);
    pins the fp64 MFMA accumulation order the regression kernels rely on. */
 int mcmc_debug_mfma_f64(mcmc_ctx* ctx, int nk, const double* A, const double* B, const double* C, double* D);
+/* The chain order the last run of `chains` launched with (regression HMC / HMCDA run their chains
+   sorted by trajectory length, slot -> local chain): *used = 1 and order[0..C) filled, or *used = 0 (identity). */
+int mcmc_debug_chains_order(mcmc_chains* chains, int32_t* used, int32_t* order);
 
 #ifdef __cplusplus
 }

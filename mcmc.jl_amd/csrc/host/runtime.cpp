@@ -110,6 +110,7 @@ struct mcmc_chains {
     DevBuf out_samples, out_grads, out_bits, out_tmp, stage_samples, stage_grads;
     DevBuf order_buf;                // regression HMC / HMCDA: chain slot -> chain (StepArgs.order)
     std::vector<int32_t> h_order;
+    bool last_order = false;         // the last run launched with order_buf (mcmc_debug_chains_order)
     // storeLeaps (HMC.jl:145-150): host buffers the next run fills (h_lpars == NULL: off), device staging
     int64_t leap_cap = 0;
     double *h_lpars = nullptr, *h_lgrads = nullptr, *h_lmom = nullptr, *h_llp = nullptr, *h_lH = nullptr;
@@ -780,6 +781,13 @@ extern "C" int mcmc_chains_reset(mcmc_chains* c) {
     return init_state(c);
 }
 
+extern "C" int mcmc_debug_chains_order(mcmc_chains* c, int32_t* used, int32_t* order) {
+    if (!c || !used) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    *used = c->last_order ? 1 : 0;
+    if (c->last_order && order) std::copy(c->h_order.begin(), c->h_order.end(), order);
+    return MCMC_OK;
+}
+
 extern "C" int mcmc_chains_evals(mcmc_chains* c, int64_t* evals) {
     if (!c || !evals) return fail(MCMC_E_INVALID_ARG, "NULL argument");
     mcmc_ctx* ctx = c->model->ctx;
@@ -1037,9 +1045,11 @@ int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs*
     const bool host_evals = evals_on_host(c);
     s.n_evals = host_evals ? nullptr : c->d_evals;
     s.order = nullptr;
+    c->last_order = false;
     if (L == LAYOUT_GLM && C > 16 && (c->sa.kind == SK_HMCDA || (c->sa.kind == SK_HMC && c->sa.tuner))) {
         if (int rc = glm_trajectory_order(c, st)) return rc;
         s.order = (const int32_t*)c->order_buf.p;
+        c->last_order = true;
     }
 
     // storeLeaps: one step per launch; before each kept step, a record launch of its trajectory

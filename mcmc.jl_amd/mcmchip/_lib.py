@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_group_chains_set_steps_per_launch", "mcmc_group_chains_block", "mcmc_group_run_serialmc",
     "mcmc_debug_group_inject_failure",
     "mcmc_seqmc_validate", "mcmc_run_seqmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox",
-    "mcmc_debug_mfma_f64",
+    "mcmc_debug_mfma_f64", "mcmc_debug_chains_order",
 )
 
 
@@ -179,6 +179,7 @@ def load() -> ct.CDLL:
         "mcmc_debug_philox": (ct.c_int, [P, i64, ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32),
                                          ct.POINTER(ct.c_uint32)]),
         "mcmc_debug_mfma_f64": (ct.c_int, [P, ct.c_int, dp, dp, dp, dp]),
+        "mcmc_debug_chains_order": (ct.c_int, [P, ct.POINTER(i32), ct.POINTER(i32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

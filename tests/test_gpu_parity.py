@@ -356,6 +356,44 @@ def test_glm_continue_and_shard(gpu):
     assert np.array_equal(np.concatenate([lo._samples, hi._samples], axis=2), full._samples)
 
 
+@pytest.mark.parametrize("sname", ["hmcda", "hmc_tuned"])
+@pytest.mark.parametrize("kind,d", [("linear", 20), ("logistic", 200)])
+def test_glm_trajectory_order_continue(gpu, sname, kind, d):
+    """Regression HMC / HMCDA launch their chains sorted by trajectory length (runtime.cpp glm_trajectory_order):
+    after an adapting run the per-chain leapStep (HMCDA) or nLeaps (tuned HMC) differ, so the continued run's tile
+    -> chain map is a real permutation; samples, gradients, accept bits, final state, evaluation counts and the
+    adapted state stay bitwise the oracle's (which knows nothing of tiles)."""
+    import ctypes as ct
+    mk = {"hmcda": lambda: mc.HMCDA(len=1.0),                # adapted leapSteps differ from chain to chain
+          "hmc_tuned": lambda: mc.HMC(2, 0.05, mc.EmpMCTuner(0.7, adaptStep=2, maxStep=9))}[sname]
+    m = _glm_model(kind, d)
+    C = 70                                                     # four full 16-chain tiles and a tail of 6
+    r1, r2 = mc.SerialMC(steps=8, burnin=6), mc.SerialMC(steps=6, burnin=1)
+    t = (m * mk() * r1).batch(C, seed=13)
+    c1 = mc.run(t)
+    ts1 = t.tuner_state()
+    t.runner = r2
+    c2 = mc.run(t)
+    used, order = ct.c_int32(0), (ct.c_int32 * C)()
+    _lib.check(_lib.load().mcmc_debug_chains_order(t.handle(), ct.byref(used), order))
+    assert used.value == 1
+    order = np.frombuffer(order, dtype=np.int32)
+    key = ts1["step"] if sname == "hmcda" else -ts1["nleaps"].astype(float)   # longest trajectory first
+    assert np.array_equal(order, np.argsort(key, kind="stable"))
+    if np.unique(key).size > 1:                               # (tuned HMC may leave every nLeaps at maxStep)
+        assert not np.array_equal(order, np.arange(C))
+    oc = orc.OracleChains(m, mk(), nchains=C, seed=13)
+    s1, g1, a1 = oc.run(r1)
+    s2, g2, a2 = oc.run(r2)
+    assert_parity(c1, s1, g1, a1, sname)
+    assert_parity(c2, s2, g2, a2, sname)
+    assert np.array_equal(c2._gradients.view(np.uint64), g2.view(np.uint64))
+    assert np.array_equal(c2.final_x.view(np.uint64), oc.x.view(np.uint64))
+    assert t.evals == int(oc.n_evals.sum())
+    ts = t.tuner_state()
+    assert np.array_equal(ts["step"].view(np.uint64), oc.t_step.view(np.uint64))
+
+
 def test_logistic_out_of_support_rejects(gpu):
     """Huge proposals push prob to exactly 0/1: log(0) -> LLAcc throws -> (-Inf, 0) -> reject."""
     X = np.hstack([np.ones((30, 1)), np.random.default_rng(1).normal(size=(30, 3)) * 30])
