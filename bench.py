@@ -392,7 +392,10 @@ def main():
     K, W = args.steps, args.warmup
     burnin = K // 10
     runner = mc.SerialMC(steps=K, burnin=burnin, thinning=args.thinning)
-    if cfg0.get("adapt") and K // 10 >= W + 2:
+    # HMCDA adapts its leapStep per chain during the burn-in (HMCDA.jl:133): config 5, and any --sampler hmcda run,
+    # warm up through that adaptation, so the timed steps run at the adapted trajectory lengths
+    adaptive = bool(cfg0.get("adapt")) or args.sampler == "hmcda"
+    if adaptive and K // 10 >= W + 2:
         sys.exit("bench.py: the timed run's burnin would reach past the adaptation warmup")
     task = mc.MCMCTask(model, sampler, runner, nchains=C, seed=1, device=local, chain_offset=rank * C,
                        steps_per_launch=max(args.spl, 0))
@@ -419,7 +422,7 @@ def main():
         # adaptive configs (config 5, HMCDA): the warmup is the configured burnin, W steps of dual averaging
         # (HMCDA.jl:133: adapts while i < burnin); the timed run continues the same chains (runners.jl:14) past
         # it, so every timed step runs at the chain's dualLeapStep (HMCDA.jl:140)
-        wr = (mc.SerialMC(steps=W + 1, burnin=W, thinning=1) if cfg0.get("adapt")
+        wr = (mc.SerialMC(steps=W + 1, burnin=W, thinning=1) if adaptive
               else mc.SerialMC(steps=W, burnin=0, thinning=1))
         wout = _lib.Outputs()
         cfg = wr.cfg()
@@ -428,7 +431,7 @@ def main():
         _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(wout)))
         torch.cuda.synchronize(dev)
         print(f"bench: warmup done in {time.perf_counter() - ta:.1f} s", file=sys.stderr, flush=True)
-        if cfg0.get("adapt"):
+        if adaptive:
             eps = task.tuner_state()["step_bar"]
             adapt = {"warmup": f"SerialMC(steps={W + 1}, burnin={W}): {W - 1} dual-averaging updates, untimed",
                      "warmup_s": time.perf_counter() - ta, "warmup_evals": task.evals,

@@ -373,7 +373,7 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
         }
         case MCMC_MODEL_LOGISTIC:
         case MCMC_MODEL_LINEAR: {
-            if (d > mcmc_glm_max_d()) return bail(fail(MCMC_E_UNSUPPORTED, "regression models support d <= 512"));
+            if (d > mcmc_glm_max_d()) return bail(fail(MCMC_E_UNSUPPORTED, "regression models support d <= 1024"));
             if (desc->n <= 0 || !desc->X || !desc->Y) return bail(fail(MCMC_E_INVALID_ARG, "regression needs n > 0, X, Y"));
             if (!(desc->prior_sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "prior sigma should be > 0"));
             if (desc->kind == MCMC_MODEL_LINEAR && !(desc->noise_sigma > 0))
@@ -1046,7 +1046,13 @@ int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs*
     s.n_evals = host_evals ? nullptr : c->d_evals;
     s.order = nullptr;
     c->last_order = false;
-    if (L == LAYOUT_GLM && C > 16 && (c->sa.kind == SK_HMCDA || (c->sa.kind == SK_HMC && c->sa.tuner))) {
+    // regression tiles run their leapfrog loop to their longest chain.  (The lane / pair layouts were measured
+    // with the same order and it did not pay: DESIGN.md §5.3.)
+    static const bool order_off = [] {                 // MCMCHIP_TRAJ_ORDER=0: identity order (A/B measurements)
+        const char* e = std::getenv("MCMCHIP_TRAJ_ORDER");
+        return e != nullptr && e[0] == '0';
+    }();
+    if (!order_off && L == LAYOUT_GLM && C > 16 && (c->sa.kind == SK_HMCDA || (c->sa.kind == SK_HMC && c->sa.tuner))) {
         if (int rc = glm_trajectory_order(c, st)) return rc;
         s.order = (const int32_t*)c->order_buf.p;
         c->last_order = true;

@@ -108,8 +108,9 @@ __device__ __forceinline__ int own_coord(const GlmPos& p, int slot) {
 }
 
 // X/Y tile buffers in LDS: the d-sliced evaluation double-buffers, the single-slice one (glm_eval1) keeps
-// three (tile t for G, t+1 for eta, t+2 being written)
-__host__ __device__ constexpr int glm_xbufs(int nw) { return nw == 1 ? 3 : 2; }
+// three (tile t for G, t+1 for eta, t+2 being written); at d_pad = 1024 one 16-row tile is 128 KB, so the
+// d-sliced evaluation keeps one (glm_eval: load and store after the tile's last reader, behind a barrier)
+__host__ __device__ constexpr int glm_xbufs(int nw, int d_pad) { return nw == 1 ? 3 : (d_pad > 512 ? 1 : 2); }
 
 // LDS carve-up (doubles): X tiles [3][16][stride] | Y tiles [3][16] | eta partials [8 waves][64][4] |
 // chain scalars [8 waves][16] | residual weights [4 tiles][4][64] | int scratch
@@ -126,8 +127,8 @@ struct GlmLds {
 __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     GlmLds L;
     L.X = smem;
-    L.Y = L.X + glm_xbufs(a.g.nw) * 16 * a.g.lds_stride;     // X tile buffers
-    L.part = L.Y + glm_xbufs(a.g.nw) * 16;
+    L.Y = L.X + glm_xbufs(a.g.nw, a.g.d_pad) * 16 * a.g.lds_stride;     // X tile buffers
+    L.part = L.Y + glm_xbufs(a.g.nw, a.g.d_pad) * 16;
     L.scal = L.part + kGlmMaxWaves * 64 * 4;
     L.rbuf = L.scal + kGlmMaxWaves * 16;
     L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
@@ -136,7 +137,7 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
 }
 
 static size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(glm_xbufs(g.nw) * 16 * g.lds_stride + glm_xbufs(g.nw) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
+    return (size_t)(glm_xbufs(g.nw, g.d_pad) * 16 * g.lds_stride + glm_xbufs(g.nw, g.d_pad) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
                     4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8;
 }
 
@@ -428,7 +429,8 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     // after it, so one barrier per tile retires both the readers of tile t and the writers of t+1.
     constexpr int kBlk = glm_block<NW>();
     constexpr int kHalf = 16 * 8 * NM * NW;                   // f64x2 per tile (d_pad = 16 NM NW)
-    constexpr int kPer = (kHalf + kBlk - 1) / kBlk;           // <= 8 for every built shape
+    constexpr int kPer = (kHalf + kBlk - 1) / kBlk;           // <= 8, 16 at d_pad = 1024 (one buffer)
+    constexpr bool kOneBuf = 16 * NM * NW > 512;              // glm_xbufs: one LDS tile buffer
     constexpr int kLgHalfrow = __builtin_ctz(8 * NM * NW);
     const int XS = 16 * S;                                    // doubles per LDS X buffer
     f64x2 buf[kPer];
@@ -458,11 +460,11 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     store_tile(0);
     __syncthreads();
     for (int64_t t = 0; t < ntiles; ++t) {
-        const int b = (int)(t & 1);
+        const int b = kOneBuf ? 0 : (int)(t & 1);
         const double* LX = L.X + b * XS;
         const double* LY = L.Y + b * 16;
         const bool more = t + 1 < ntiles;
-        if (more) load_tile(t + 1);
+        if (more && !kOneBuf) load_tile(t + 1);
         // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e
         f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
         const double* xrow = LX + p.cl * S + p.base + 4 * p.q;
@@ -537,7 +539,15 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
                 }
             }
         }
-        if (more) store_tile(b ^ 1);                          // the other buffer: its readers finished tile t-1
+        if (kOneBuf) {                                        // the one buffer: after its last reader of tile t
+            __syncthreads();
+            if (more) {
+                load_tile(t + 1);
+                store_tile(0);
+            }
+        } else if (more) {
+            store_tile(b ^ 1);                                // the other buffer: its readers finished tile t-1
+        }
         __syncthreads();
     }
     return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, lik_part, oos);
@@ -1608,18 +1618,22 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
 
 mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
     // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1);
-    // 128 < d <= 512: NW = 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW.
+    // 128 < d <= 512: NW = 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW;
+    // 512 < d <= 1024: NW = 8 waves of DS = 128 (NM = 8), d_pad = 1024, one LDS tile buffer (glm_xbufs).
     mcmc::GlmShape g{};
     if (d <= 128) {
         int nm = 1;
         while (16 * nm < d) nm *= 2;
         g.nw = 1;
         g.nm = nm;
-    } else {
+    } else if (d <= 512) {
         int nw = 2;
         while (64 * nw < d) nw *= 2;
         g.nw = nw;
         g.nm = 4;
+    } else {
+        g.nw = 8;
+        g.nm = 8;
     }
     g.ds = 16 * g.nm;
     g.d_pad = g.ds * g.nw;
@@ -1629,7 +1643,7 @@ mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
     return g;
 }
 
-int mcmc_glm_max_d() { return 512; }
+int mcmc_glm_max_d() { return 1024; }
 
 // steps one launch of the regression step kernel may fuse (0: any): the single-slice MALA kernel is a
 // one-step kernel (glm_mala1)
@@ -1687,6 +1701,7 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& k, hipStream_t st) {
         case 81: return glm_step_nm<8, 1>(a, lds, grid, st);
         case 44: return glm_step_nm<4, 4>(a, lds, grid, st);
         case 48: return glm_step_nm<4, 8>(a, lds, grid, st);
+        case 88: return glm_step_nm<8, 8>(a, lds, grid, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1715,6 +1730,7 @@ hipError_t mcmc_launch_glm_record(const mcmc::KernelArgs& k, const mcmc::LeapRec
         case 81: return glm_rec_nm<8, 1>(a, lds, grid, st);
         case 44: return glm_rec_nm<4, 4>(a, lds, grid, st);
         case 48: return glm_rec_nm<4, 8>(a, lds, grid, st);
+        case 88: return glm_rec_nm<8, 8>(a, lds, grid, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1733,6 +1749,7 @@ hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& k, const double* xin, do
         case 81: glm_eval_kernel<8, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
         case 44: glm_eval_kernel<4, 4><<<grid, glm_block<4>(), lds, st>>>(a, xin, lp, g, check); break;
         case 48: glm_eval_kernel<4, 8><<<grid, glm_block<8>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 88: glm_eval_kernel<8, 8><<<grid, glm_block<8>(), lds, st>>>(a, xin, lp, g, check); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

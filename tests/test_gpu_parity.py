@@ -316,7 +316,7 @@ GLM_SAMPLERS = {
 
 @pytest.mark.parametrize("sname", list(GLM_SAMPLERS))
 @pytest.mark.parametrize("kind", ["logistic", "linear"])
-@pytest.mark.parametrize("d", [3, 16, 37, 64, 100, 200, 300])
+@pytest.mark.parametrize("d", [3, 16, 37, 64, 100, 200, 300, 600, 1024])     # 600, 1024: 8 slices of 128, one X buffer
 def test_glm_sampler_parity(gpu, sname, kind, d):
     m = _glm_model(kind, d)
     C = 40                                               # not a multiple of 16: tail tile
@@ -330,13 +330,20 @@ def test_glm_sampler_parity(gpu, sname, kind, d):
 
 
 @pytest.mark.parametrize("kind", ["logistic", "linear"])
-@pytest.mark.parametrize("d", [10, 130])
+@pytest.mark.parametrize("d", [10, 130, 700])
 def test_glm_eval_matches_oracle(gpu, kind, d):
     m = _glm_model(kind, d, n=70)
     x = np.random.default_rng(3).normal(size=(d, 37)) * 0.2
     lp, g = m.evalallg(x)
     lp_r, g_r = orc.eval_batch(m, x)
     assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
+
+
+def test_glm_width_cap(gpu):
+    """d = 1024 is the widest regression shape (8 slices of 128 coordinates, one 128 KB X tile in LDS); wider models
+    are refused at model() with the cap in the message."""
+    with pytest.raises(Exception, match="d <= 1024"):
+        _glm_model("linear", 1025, n=20).evalallg(np.zeros((1025, 1)))
 
 
 def test_glm_continue_and_shard(gpu):
