@@ -218,8 +218,11 @@ def measured_fp64(kname, wkey):
 
     def shape(key):                      # per-evaluation work does not depend on the step count or thinning
         return "|".join(f for f in (key or "").split("|") if not f.startswith(("steps=", "thinning=")))
+    def kern(name):                      # the profile's glm_hmc<NM, NW, DA, REC> is the run's glm_hmc<NM, NW, DA>
+        n = _norm_kernel(name)
+        return n[:-len(",false>")] + ">" if n.startswith("glm_hmc<") and n.count(",") == 3 and n.endswith(",false>") else n
     for k, e in json.load(open(p)).items():
-        if (_norm_kernel(e.get("kernel", k)) == _norm_kernel(kname) and e.get("src_hash") == h
+        if (kern(e.get("kernel", k)) == kern(kname) and e.get("src_hash") == h
                 and shape(e.get("workload_key")) == shape(wkey)):
             return e
     return None
