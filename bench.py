@@ -551,6 +551,34 @@ def main():
                 "note": "the same workload with host output buffers: the step loop plus the device-to-host copy "
                         "of the kept outputs after it"}
         del hs, hg, hb
+    gather = None
+    if dist is not None and world > 1:
+        # the end-of-run gather, after and apart from the timed region: the timed run's kept
+        # samples (+ gradients), accept bits chunked point to point into rank 0's host memory (sharded.py
+        # gather_shards); capped at GATHER_CAP_BYTES of global samples so a 1000-step 8-GPU metric run does not
+        # fill the host (the kept rows gathered are then the first `rows` of each rank)
+        from mcmchip.sharded import gather_shards
+        GATHER_CAP_BYTES = 32 << 30
+        row_bytes = d * C * 8 * world * (2 if grads is not None else 1)
+        rows = max(1, min(nkept, GATHER_CAP_BYTES // max(1, row_bytes)))
+        gparts = {"samples": samples[:rows], "accept_bits": bits[:rows]}
+        if grads is not None:
+            gparts["gradients"] = grads[:rows]
+        if backend != "nccl":
+            gparts = {k: v.cpu() for k, v in gparts.items()}
+        gstats = {}
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tg = time.perf_counter()
+        g_out = gather_shards(gparts, C, C, C * world, dst=0, stats=gstats)
+        gmax = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(gmax, op=dist.ReduceOp.MAX)
+        gbytes = sum(v.numel() * v.element_size() for v in gparts.values()) * world
+        gather = {"gather_s": float(gmax[0]), "bytes": int(gbytes), "GB_per_s": gbytes / float(gmax[0]) / 1e9,
+                  "kept_rows": rows, "of_kept_rows": nkept, "max_recv_buffer_bytes": gstats.get("max_recv_buffer_bytes"),
+                  "note": "chunked point-to-point gather of the timed run's outputs into rank 0's host memory, "
+                          "timed apart (max over ranks); never inside the step loop"}
+        del g_out, gparts
     spl = args.spl if args.spl >= 0 else 0
     nl = ct.c_int64(0)
     _lib.check(lib.mcmc_chains_launches(h, K, ct.byref(nl)))
@@ -671,6 +699,8 @@ def main():
         line["reference_units"] = binomial_units(mc, model, C, local)
     if pcie is not None:
         line["pcie_inclusive"] = pcie
+    if gather is not None:
+        line["gather"] = gather
     if rank == 0 and not args.no_cpu_baseline:          # after the timed region, also on N > 1 lines
         lps = evals / (C * K) if args.sampler == "hmcda" else None
         line["cpu_baseline"] = cpu_baseline(model, sampler, args.cpu_seconds,

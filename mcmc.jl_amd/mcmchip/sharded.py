@@ -37,39 +37,99 @@ def shard(nchains: int, world: int, rank: int, align: int = 64):
     return off, min(block, nchains - off), block
 
 
-def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None, dst: int = 0):
-    """Gather per-rank arrays whose LAST axis is the rank's chain block onto `dst`.
+DEFAULT_CHUNK_BYTES = 256 << 20
 
-    parts: name -> torch tensor [..., count] (accept bits: [..., ceil(count/64)] words).  Every rank pads its
-    block to `block` chains, one torch.distributed.gather per array; on dst returns name -> numpy array over
-    all `nchains` chains (bits: ceil(nchains/64) words), elsewhere None."""
+
+def _host_empty(shape, dtype, pin):
+    """Destination host array (numpy view of a torch tensor, page-locked when the transfers come from a GPU)."""
+    import torch
+    if pin:
+        try:
+            return torch.empty(shape, dtype=dtype, pin_memory=True)
+        except RuntimeError:            # page-locking refused (size, limits): pageable memory still works
+            pass
+    return torch.empty(shape, dtype=dtype)
+
+
+def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None, dst: int = 0,
+                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, stats: Optional[dict] = None):
+    """Gather per-rank arrays whose LAST axis is the rank's chain block into host memory on `dst`.
+
+    parts: name -> torch tensor [..., count] (accept bits: [..., ceil(count/64)] words), on the rank's GPU
+    (NCCL) or on the host (gloo).  Rank r's columns are the global chains shard(nchains, world, r).  The
+    transfer is point to point, rank by rank and chunk by chunk: a chunk is a run of whole leading rows
+    (e.g. kept steps) of at most `chunk_bytes`, sent by its rank and received on `dst` into ONE reused
+    buffer, then copied straight into the destination's host array.  So `dst` never holds more than one
+    chunk of another rank's data on its device (the world's outputs are never concatenated on one GPU:
+    at the 8-GPU metric they would be 193 GB).  Returns name -> numpy array over all `nchains` chains
+    (bits: ceil(nchains/64) words) on dst, None elsewhere.  `stats` (a dict, dst only) receives
+    `max_recv_buffer_bytes` and `bytes` (bytes received from other ranks)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if chunk_bytes <= 0:
+        raise ValueError("chunk_bytes must be > 0")
+    on_gpu = dist.get_backend(group) == "nccl"
     out = {} if rank == dst else None
+    max_buf = 0
+    moved = 0
     for name, t in parts.items():
         is_bits = name == "accept_bits"
-        width = (block // 64) if is_bits else block
-        have = t.shape[-1]
-        padded = torch.zeros(t.shape[:-1] + (width,), dtype=t.dtype, device=t.device)
-        padded[..., :have] = t
-        bucket = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
-        dist.gather(padded, bucket, dst=dst, group=group)
+        lead = tuple(t.shape[:-1])
+        rows = 1
+        for n in lead:
+            rows *= n
+        esize = t.element_size()
+        keep = (nchains + 63) // 64 if is_bits else nchains
+        host = None
         if rank == dst:
-            full = torch.cat(bucket, dim=-1)
-            keep = (nchains + 63) // 64 if is_bits else nchains
-            out[name] = full[..., :keep].cpu().numpy()
+            host = _host_empty((rows, keep), t.dtype, on_gpu and torch.cuda.is_available())
+        buf = None
+        for r in range(world):
+            off, cnt, _ = shard(nchains, world, r)
+            if cnt <= 0:
+                continue
+            woff = off // 64 if is_bits else off
+            width = (cnt + 63) // 64 if is_bits else cnt
+            per = max(1, chunk_bytes // max(1, width * esize))
+            if r == rank:
+                mine = t.reshape(rows, t.shape[-1])[:, :width]
+                if rank == dst:
+                    host[:, woff:woff + width].copy_(mine)
+                else:
+                    for r0 in range(0, rows, per):
+                        dist.send(mine[r0:r0 + per].contiguous(), dst=dist.get_global_rank(group, dst)
+                                  if group is not None else dst, group=group)
+            elif rank == dst:
+                src = dist.get_global_rank(group, r) if group is not None else r
+                for r0 in range(0, rows, per):
+                    n = min(per, rows - r0)
+                    need = n * width
+                    if buf is None or buf.numel() < need:
+                        buf = torch.empty(max(need, min(rows, per) * width), dtype=t.dtype, device=t.device)
+                        max_buf = max(max_buf, buf.numel() * esize)
+                    view = buf[:need].view(n, width)
+                    dist.recv(view, src=src, group=group)
+                    host[r0:r0 + n, woff:woff + width].copy_(view)
+                    moved += need * esize
+        buf = None
+        if rank == dst:
+            out[name] = host.numpy().reshape(lead + (keep,))
+    if stats is not None and rank == dst:
+        stats["max_recv_buffer_bytes"] = max_buf
+        stats["bytes"] = moved
     return out
 
 
 def run_sharded(model, sampler, runner: SerialMC, nchains: int, seed: int = 1, group=None, dst: int = 0,
-                device: Optional[int] = None) -> Optional[MCMCChain]:
+                device: Optional[int] = None, chunk_bytes: int = DEFAULT_CHUNK_BYTES) -> Optional[MCMCChain]:
     """run(model * sampler * runner) over `nchains` chains split across the ranks of `group`.
 
     Call on every rank (torch.distributed initialised; one GPU per rank: `device` defaults to the rank's
     LOCAL_RANK).  Returns the assembled MCMCChain on `dst`, None elsewhere.  chain.runTime is the step loop's
-    wall time (max over ranks); chain.gather_s the end-of-run gather."""
+    wall time (max over ranks); chain.gather_s the end-of-run gather (chunked point to point into host memory
+    on `dst`, gather_shards), chain.gather_stats its bytes and largest receive buffer."""
     import os
     import torch
     import torch.distributed as dist
@@ -108,7 +168,8 @@ def run_sharded(model, sampler, runner: SerialMC, nchains: int, seed: int = 1, g
     rt = torch.tensor([runtime], dtype=torch.float64, device=dev if dist.get_backend(group) == "nccl" else "cpu")
     dist.all_reduce(rt, op=dist.ReduceOp.MAX, group=group)
     t0 = time.perf_counter()
-    full = gather_shards(parts, cnt, block, nchains, group=group, dst=dst)
+    gstats = {}
+    full = gather_shards(parts, cnt, block, nchains, group=group, dst=dst, chunk_bytes=chunk_bytes, stats=gstats)
     gather_s = time.perf_counter() - t0
     if rank != dst:
         return None
@@ -118,4 +179,5 @@ def run_sharded(model, sampler, runner: SerialMC, nchains: int, seed: int = 1, g
     ch = MCMCChain(runner.r, full["samples"], full.get("gradients"), diags, whole, float(rt[0]),
                    final_x=full["final_x"], final_lp=full["final_lp"])
     ch.gather_s = gather_s
+    ch.gather_stats = gstats
     return ch

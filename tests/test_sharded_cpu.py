@@ -52,7 +52,7 @@ def _fake_shard(off, cnt, nk, d):
     return samples, acc, words
 
 
-def _worker(rank, world, port, total, nk, d, q):
+def _worker(rank, world, port, total, nk, d, q, chunk=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -60,22 +60,29 @@ def _worker(rank, world, port, total, nk, d, q):
         s, _, words = _fake_shard(off, cnt, nk, d)
         parts = {"samples": torch.from_numpy(s), "accept_bits": torch.from_numpy(words.view(np.int64)),
                  "final_lp": torch.from_numpy(s[-1, 0].copy())}
-        full = gather_shards(parts, cnt, block, total, dst=0)
+        stats = {}
+        kw = {} if chunk is None else {"chunk_bytes": chunk}
+        full = gather_shards(parts, cnt, block, total, dst=0, stats=stats, **kw)
         if rank == 0:
-            q.put({k: v.copy() for k, v in full.items()})
+            res = {k: v.copy() for k, v in full.items()}
+            res["_stats"] = stats
+            q.put(res)
         else:
             q.put(None if full is None else "unexpected")
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("total", [130, 1000])
-def test_gather_shards_gloo_world2(total):
+@pytest.mark.parametrize("total,chunk", [(130, None), (1000, None), (1000, 8 * 500 * 2), (777, 64)])
+def test_gather_shards_gloo_world2(total, chunk):
+    """The chunked point-to-point gather reassembles every array exactly, whatever the chunk size (64 B: one
+    row per message), and the destination's receive buffer never exceeds one chunk (one row when a row is
+    larger than the chunk)."""
     nk, d, world = 3, 2, 2
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, total, nk, d, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, nk, d, q, chunk)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -88,3 +95,8 @@ def test_gather_shards_gloo_world2(total):
     assert np.array_equal(full["samples"], s)
     assert np.array_equal(full["final_lp"], s[-1, 0])
     assert np.array_equal(full["accept_bits"].view(np.uint64), words)
+    st = full["_stats"]
+    _, cnt1, _ = shard(total, world, 1)
+    assert st["bytes"] == 8 * cnt1 * (nk * d + 1) + 8 * nk * ((cnt1 + 63) // 64)
+    if chunk is not None:
+        assert st["max_recv_buffer_bytes"] <= max(chunk, 8 * cnt1)
