@@ -266,6 +266,10 @@ int mcmc_group_chains_block(mcmc_group_chains* gc, int32_t g, mcmc_chains** chai
  * mcmc_group_chains_reset: the blocks may then be at different steps. */
 int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_cfg* runner, mcmc_outputs* out,
                             double* gather_s);
+/* the last mcmc_group_run_serialmc's page-locking of the caller's output buffers (hipHostRegister before,
+ * hipHostUnregister after; 0 when they were pinned already), in seconds.  It is not part of gather_s, which
+ * times the copies alone: a caller that runs once into fresh pageable buffers pays both. */
+int mcmc_group_last_pin_s(const mcmc_group_chains* gc, double* pin_s);
 /* test hook: the next mcmc_group_run_serialmc fails block `block` before it starts (the others run) */
 int mcmc_debug_group_inject_failure(mcmc_group_chains* gc, int32_t block);
 

@@ -36,6 +36,7 @@ struct mcmc_group_chains {
     bool failed = false;
     std::string fail_msg;
     int32_t inject_fail = -1;        // mcmc_debug_group_inject_failure: this block's next run fails before it starts
+    double last_pin_s = 0.0;         // the last run's page-locking of the caller's outputs (register + release)
 };
 
 static int bad(const char* msg) { return mcmc_set_error(MCMC_E_INVALID_ARG, msg); }
@@ -196,6 +197,8 @@ extern "C" int mcmc_group_chains_block(mcmc_group_chains* gc, int32_t b, mcmc_ch
 // registered (portable: visible to every device's copy engine) for the duration of the run and released after
 // it.  Device -> host copies into pageable memory are staged through a driver bounce buffer at a fraction of
 // the link rate; into pinned memory they are direct DMA.
+// reg_s: the registration plus (release()) the unregistration time, reported apart from the copies
+// (mcmc_group_last_pin_s): at the metric size it is comparable to the gather itself.
 struct PinnedOutputs {
     std::vector<void*> registered;
     double reg_s = 0.0;
@@ -206,9 +209,13 @@ struct PinnedOutputs {
         else (void)hipGetLastError();           // already pinned (hipErrorHostMemoryAlreadyRegistered) or not
                                                 // registrable: the copy still works, staged
     }
-    ~PinnedOutputs() {
+    void release() {
+        const auto c0 = std::chrono::steady_clock::now();
         for (void* p : registered) (void)hipHostUnregister(p);
+        registered.clear();
+        reg_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
     }
+    ~PinnedOutputs() { release(); }
 };
 
 extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_cfg* r, mcmc_outputs* out,
@@ -280,6 +287,8 @@ extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_
         gc->fail_msg = "could not start a worker thread";
         return mcmc_set_error(MCMC_E_HIP, "mcmc_group_run_serialmc: could not start a worker thread");
     }
+    pins.release();
+    gc->last_pin_s = pins.reg_s;
     double rt = 0.0, kms = 0.0, gs = 0.0;
     for (int32_t b : blocks) {
         if (res[b].rc) {
@@ -299,6 +308,12 @@ extern "C" int mcmc_group_run_serialmc(mcmc_group_chains* gc, const mcmc_runner_
         out->nkept = res[blocks.back()].o.nkept;
     }
     if (gather_s) *gather_s = gs;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_group_last_pin_s(const mcmc_group_chains* gc, double* pin_s) {
+    if (!gc || !pin_s) return bad("NULL argument");
+    *pin_s = gc->last_pin_s;
     return MCMC_OK;
 }
 

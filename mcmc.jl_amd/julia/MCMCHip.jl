@@ -91,11 +91,13 @@ end
 # mcmc_group_*: contiguous 64-chain-aligned blocks, one per listed device, driven from this one Julia thread
 # (a library worker thread per block); results bit-identical to one context running every chain.  Blocks are whole
 # 64-chain groups, so a batch of fewer than 64 N chains leaves trailing devices idle.  The handles are freed by
-# finalizers (or destroy! explicitly); a GroupChains keeps its Group alive, so the group is destroyed after them.
+# finalizers (or destroy! explicitly); a group whose chains are still alive is kept (the library refuses it) and released
+# by the destroy! of its last GroupChains, whatever order the finalizers run in.
 mutable struct Group
     h::Ptr{Cvoid}
+    released::Bool                 # destroy! was called (explicitly or by the finalizer)
     function Group(h)
-        g = new(h)
+        g = new(h, false)
         finalizer(destroy!, g)
     end
 end
@@ -110,10 +112,20 @@ end
 function destroy!(gc::GroupChains)
     gc.h == C_NULL || ccall((:mcmc_group_chains_destroy, lib), Cint, (Ptr{Cvoid},), gc.h)
     gc.h = C_NULL
+    # Julia does not order the finalizers of objects collected in one cycle: if the group's ran first, the library
+    # refused it (chains alive) and the group kept its handle; with these chains gone, release it now
+    gc.group.released && release_group!(gc.group)
+    nothing
+end
+function release_group!(g::Group)
+    g.h == C_NULL && return
+    # refused while any GroupChains of the group is alive: keep the handle, the last one retries
+    ccall((:mcmc_group_destroy, lib), Cint, (Ptr{Cvoid},), g.h) == 0 && (g.h = C_NULL)
+    nothing
 end
 function destroy!(g::Group)
-    g.h == C_NULL || ccall((:mcmc_group_destroy, lib), Cint, (Ptr{Cvoid},), g.h)
-    g.h = C_NULL
+    g.released = true
+    release_group!(g)
 end
 
 function device_count()

@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = (
     "mcmc_group_create", "mcmc_group_destroy", "mcmc_group_size", "mcmc_group_plan", "mcmc_group_chains_create",
     "mcmc_group_chains_destroy", "mcmc_group_chains_reset", "mcmc_group_chains_steps_done",
     "mcmc_group_chains_set_steps_per_launch", "mcmc_group_chains_block", "mcmc_group_run_serialmc",
+    "mcmc_group_last_pin_s",
     "mcmc_debug_group_inject_failure",
     "mcmc_seqmc_validate", "mcmc_run_seqmc", "mcmc_stats_ess", "mcmc_debug_detmath", "mcmc_debug_philox",
     "mcmc_debug_mfma_f64", "mcmc_debug_chains_order",
@@ -169,6 +170,7 @@ def load() -> ct.CDLL:
         "mcmc_group_chains_block": (ct.c_int, [P, i32, pp, ct.POINTER(i64), ct.POINTER(i64)]),
         "mcmc_group_run_serialmc": (ct.c_int, [P, ct.POINTER(RunnerCfg), ct.POINTER(Outputs),
                                                ct.POINTER(ct.c_double)]),
+        "mcmc_group_last_pin_s": (ct.c_int, [P, ct.POINTER(ct.c_double)]),
         "mcmc_debug_group_inject_failure": (ct.c_int, [P, i32]),
         "mcmc_seqmc_validate": (ct.c_int, [ct.c_void_p]),
         "mcmc_run_seqmc": (ct.c_int, [ct.POINTER(ct.c_void_p), i32, i64, ct.c_void_p, ct.c_void_p, u64, i32,

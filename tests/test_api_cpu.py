@@ -213,3 +213,54 @@ def test_bench_valu_roofline_profile():
         cyc = 4 * e["valu_quadcycles_per_chain_step"] * chains * steps       # VALU issue cycles of the launch
         frac_at_clock = cyc / e["duration_s"] / (1024 * e["clock_ghz"] * 1e9)
         assert 0.3 < frac_at_clock <= 1.0 + 1e-6, (k, frac_at_clock)
+
+
+def _c_struct_fields(name):
+    """(field, julia type) of a typedef struct in include/mcmc_hip.h, in order."""
+    import re
+    h = open(os.path.join(ROOT, "include", "mcmc_hip.h")).read()
+    body = re.search(r"typedef struct \{([^{}]*)\}\s*" + name + ";", h).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    ty = {"int32_t": "Int32", "int64_t": "Int64", "double": "Float64", "double*": "Ptr{Float64}",
+          "uint64_t*": "Ptr{UInt64}"}
+    out = []
+    for decl in body.split(";"):
+        decl = decl.replace("const ", "").strip()
+        if not decl:
+            continue
+        m = re.match(r"(\w+\s*\*?)\s*(.*)", decl)
+        base = m.group(1).replace(" ", "")
+        for nm in m.group(2).split(","):
+            nm = nm.strip()
+            t = base
+            if nm.startswith("*"):
+                nm, t = nm[1:].strip(), base + "*"
+            out.append((nm, ty[t]))
+    return out
+
+
+def _jl_struct_fields(path, jname):
+    import re
+    s = open(path).read()
+    body = re.search(r"(?:immutable|type|struct|mutable struct)\s+" + jname + r"\b(.*?)\bend\b", s,
+                     flags=re.S).group(1)
+    body = re.sub(r"#[^\n]*", "", body)
+    fields = []
+    for part in re.split(r"[;\n]", body):
+        part = part.strip()
+        if part:
+            nm, t = part.split("::")
+            fields.append((nm.strip(), t.strip().replace("Uint64", "UInt64")))
+    return fields
+
+
+@pytest.mark.parametrize("c_name,hook_name,plain_name", [
+    ("mcmc_model_desc", "HipModelDesc", "ModelDesc"), ("mcmc_sampler_cfg", "HipSamplerCfg", "SamplerCfg"),
+    ("mcmc_runner_cfg", "HipRunnerCfg", "RunnerCfg"), ("mcmc_outputs", "HipOutputs", "Outputs")])
+def test_julia_hook_structs_mirror_header(c_name, hook_name, plain_name):
+    """Both Julia bindings (the MCMC.jl hook for the reference's Julia, MCMCHip.jl for Julia >= 1.0) declare the
+    C structs field for field: same names, order and types (there is no Julia in the image to compile them)."""
+    jdir = os.path.join(ROOT, "mcmc.jl_amd", "julia")
+    c = _c_struct_fields(c_name)
+    assert _jl_struct_fields(os.path.join(jdir, "mcmc_jl_hook.jl"), hook_name) == c
+    assert _jl_struct_fields(os.path.join(jdir, "MCMCHip.jl"), plain_name) == c

@@ -244,8 +244,12 @@ def test_group_gather_rate_at_metric_size(gpu):
     _lib.check(lib.mcmc_group_run_serialmc(h, ct.byref(cfg), ct.byref(out), ct.byref(gs)))
     wall = time.perf_counter() - t0
     nbytes = samples.nbytes + bits.nbytes
+    pin = ct.c_double(-1.0)
+    _lib.check(lib.mcmc_group_last_pin_s(h, ct.byref(pin)))
+    assert pin.value >= 0.0
     line = {"test": "group_gather", "chains": C, "d": d, "kept": nk, "blocks": 2, "bytes": nbytes,
-            "gather_s": gs.value, "gather_GBps": nbytes / gs.value / 1e9, "step_loop_s": out.runtime_s,
+            "gather_s": gs.value, "gather_GBps": nbytes / gs.value / 1e9, "pin_s": pin.value,
+            "gather_with_pin_GBps": nbytes / (gs.value + pin.value) / 1e9, "step_loop_s": out.runtime_s,
             "call_wall_s": wall}
     print(json.dumps(line))
     assert np.isfinite(samples[-1]).all() and samples[-1, :, ::65536].std() > 0
