@@ -24,7 +24,7 @@ struct ModelArgs {
     double link_sign;           // LOGISTIC
     int64_t n;                  // observations
     int64_t n_pad;              // observations padded to the MFMA tile
-    const double* X;            // [n_pad][d] row-major (zero rows past n)
+    const double* X;            // regression: the staged-tile image of X and Y (glm_layout.hpp)
     const double* Y;            // [n_pad]
     const double* init;         // [d]
 };

@@ -384,14 +384,12 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
                 for (int64_t i = 0; i < desc->n; ++i)
                     if (!(desc->Y[i] == 0.0 || desc->Y[i] == 1.0))
                         return bail(fail(MCMC_E_INVALID_ARG, "logistic responses must be 0 or 1 (Bernoulli)"));
-            // X_pad [n_pad][d_pad] row-major, zero rows/columns past (n, d) (glm.hip geometry)
-            const int64_t d_pad = mcmc_glm_d_pad((int)d);
+            // the kernels' staged-tile image of X and Y (glm_layout.hpp: 16-row tiles in the LDS layout, Y inside
+            // each tile, zero padding), plus Y [n_pad] on its own
             const int64_t n_pad = (desc->n + 15) / 16 * 16;
-            std::vector<double> Xp((size_t)n_pad * d_pad, 0.0), Yp((size_t)n_pad, 0.0);
-            for (int64_t i = 0; i < desc->n; ++i) {
-                for (int64_t k = 0; k < d; ++k) Xp[(size_t)i * d_pad + k] = desc->X[(size_t)i * d + k];
-                Yp[(size_t)i] = desc->Y[i];
-            }
+            std::vector<double> Xp(mcmc_glm_image_doubles((int)d, desc->n)), Yp((size_t)n_pad, 0.0);
+            mcmc_glm_pack_image((int)d, desc->n, desc->X, desc->Y, Xp.data());
+            for (int64_t i = 0; i < desc->n; ++i) Yp[(size_t)i] = desc->Y[i];
             if (int r = dmalloc(&m->d_X, Xp.size())) return bail(r);
             if (int r = dmalloc(&m->d_Y, Yp.size())) return bail(r);
             if (h2d(ctx, m->d_X, Xp.data(), Xp.size() * 8) != hipSuccess ||

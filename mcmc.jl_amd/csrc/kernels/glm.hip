@@ -20,9 +20,12 @@
 // fma chain over coordinates in (m, e, q) order per slice, slices added left to right; G is an fma
 // chain over observations; per-coordinate sums are lane partials in (m, e) order combined as
 // (q0 + q2) + (q1 + q3), then slices left to right.
+#include <cstdlib>
+
 #include "../common.hpp"
 #include "../detmath.hpp"
 #include "../models.hpp"
+#include "../glm_layout.hpp"
 #include "../ram.hpp"
 #include "../host/kernels_api.hpp"
 
@@ -31,9 +34,9 @@ namespace mcmc {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
-// workgroup: max(4, NW) waves = (4 / NW) tiles of 16 chains, or one tile when NW = 8
+// workgroup: one slice (NW = 1): 4 waves = 4 tiles of 16 chains; d-sliced (NW = 2, 4, 8): 8 waves = 8 / NW tiles
 template <int NW>
-constexpr int glm_block() { return 64 * (NW > 4 ? NW : 4); }
+constexpr int glm_block() { return NW == 1 ? 256 : 512; }
 constexpr int kGlmMaxWaves = 8;
 // glm_eval1's elementwise schedule (the same operations either way): each sub-stage between
 // eta MFMAs runs one stage of one observation row (0) or of all four rows of the lane (1)
@@ -65,7 +68,8 @@ struct GlmShape {
     int ds;          // coordinates per wave
     int nm;          // ds / 16
     int d_pad;
-    int lds_stride;  // X tile row stride in LDS (doubles)
+    int lds_stride;  // X tile row stride (doubles), glm_row_stride(d_pad)
+    int ts;          // doubles per staged tile (rows, then Y), glm_tile_doubles(d_pad)
     int64_t n_pad;
 };
 
@@ -107,16 +111,16 @@ __device__ __forceinline__ int own_coord(const GlmPos& p, int slot) {
     return p.base + 16 * (slot >> 2) + 4 * p.q + (slot & 3);
 }
 
-// X/Y tile buffers in LDS: the d-sliced evaluation double-buffers, the single-slice one (glm_eval1) keeps
-// three (tile t for G, t+1 for eta, t+2 being written); at d_pad = 1024 one 16-row tile is 128 KB, so the
-// d-sliced evaluation keeps one (glm_eval: load and store after the tile's last reader, behind a barrier)
+// tile buffers in LDS (each glm_tile_doubles: 16 X rows in the glm_layout.hpp image, then Y): the d-sliced
+// evaluation double-buffers, the single-slice one (glm_eval1) keeps three (tile t for G, t+1 for eta, t+2 being
+// written); at d_pad = 1024 one tile is 129 KB, so the d-sliced evaluation keeps one (glm_eval: staged after the
+// tile's last reader, behind a barrier)
 __host__ __device__ constexpr int glm_xbufs(int nw, int d_pad) { return nw == 1 ? 3 : (d_pad > 512 ? 1 : 2); }
 
-// LDS carve-up (doubles): X tiles [3][16][stride] | Y tiles [3][16] | eta partials [8 waves][64][4] |
-// chain scalars [8 waves][16] | residual weights [4 tiles][4][64] | int scratch
+// LDS carve-up (doubles): tiles [xbufs][ts] | eta partials [8 waves][64][4] | chain scalars [8 waves][16] |
+// residual weights [4 tiles][4][64] | int scratch
 struct GlmLds {
     double* X;
-    double* Y;
     double* part;
     double* scal;
     double* rbuf;     // [4 tiles][4 r][64 lanes]: residual weights of a tile, exchanged between slice waves
@@ -127,8 +131,7 @@ struct GlmLds {
 __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     GlmLds L;
     L.X = smem;
-    L.Y = L.X + glm_xbufs(a.g.nw, a.g.d_pad) * 16 * a.g.lds_stride;     // X tile buffers
-    L.part = L.Y + glm_xbufs(a.g.nw, a.g.d_pad) * 16;
+    L.part = L.X + glm_xbufs(a.g.nw, a.g.d_pad) * a.g.ts;                 // tile buffers
     L.scal = L.part + kGlmMaxWaves * 64 * 4;
     L.rbuf = L.scal + kGlmMaxWaves * 16;
     L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
@@ -137,7 +140,7 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
 }
 
 static size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(glm_xbufs(g.nw, g.d_pad) * 16 * g.lds_stride + glm_xbufs(g.nw, g.d_pad) * 16 + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
+    return (size_t)(glm_xbufs(g.nw, g.d_pad) * g.ts + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
                     4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8;
 }
 
@@ -228,7 +231,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
                                                 const XA& x, f64x4 (&G)[NM]) {
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
-    const int S = g.lds_stride;
+    constexpr int S = glm_row_stride(16 * NM);
     const double sgn = M.link_sign;
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = LOGI ? 0.0 : det_log(sn);
@@ -236,40 +239,38 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
     double lik_part = 0.0;
     const int64_t ntiles = g.n_pad / 16;
     constexpr int kBlk = glm_block<1>();
-    constexpr int kHalf = 16 * 8 * NM;                        // f64x2 per tile (d_pad = 16 NM)
+    constexpr int DP = 16 * NM;
+    constexpr int XS = glm_tile_doubles(DP);                  // one staged tile: X rows, then Y
+    constexpr int YO = glm_y_offset(DP);
+    constexpr int kHalf = XS / 2;                             // f64x2 per tile
     constexpr int kPer = (kHalf + kBlk - 1) / kBlk;
-    constexpr int kLgHalfrow = __builtin_ctz(8 * NM);
-    const int XS = 16 * S;
+    static_assert(glm_row_stride(DP) > 0, "");
     f64x2 buf[kPer];
-    double ytile = 0.0;
+    // the tile image moves linearly (glm_layout.hpp): HBM tile tt -> LDS buffer b
     auto load_tile = [&](int64_t tt) {
-        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * 16 * g.d_pad);
+        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * XS);
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
             const int i = threadIdx.x + kBlk * j;
             buf[j] = src[i < kHalf ? i : 0];
         }
-        ytile = (threadIdx.x < 16) ? M.Y[tt * 16 + threadIdx.x] : 0.0;
     };
     auto store_tile = [&](int b) {
-        double* Xb = L.X + b * XS;
+        f64x2* dst = reinterpret_cast<f64x2*>(L.X + b * XS);
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
             const int i = threadIdx.x + kBlk * j;
-            if (i < kHalf) {
-                const int row = i >> kLgHalfrow, col = 2 * (i & ((1 << kLgHalfrow) - 1));
-                *reinterpret_cast<f64x2*>(&Xb[row * S + col]) = buf[j];
-            }
+            if (i < kHalf) dst[i] = buf[j];
         }
-        if (threadIdx.x < 16) L.Y[b * 16 + threadIdx.x] = ytile;
     };
+    const int eta_lane = p.cl * S + 4 * p.q;              // + glm_eta_off(slot): coordinate 16m + 4q + e
     // eta of the tile in buffer b: k-slice kk = 4m + e, row q <-> coordinate 16m + 4q + e
     auto eta_of = [&](int b) {
         f64x4 e = f64x4{0.0, 0.0, 0.0, 0.0};
-        const double* xrow = L.X + b * XS + p.cl * S + 4 * p.q;
+        const double* xrow = L.X + b * XS + eta_lane;
 #pragma unroll
         for (int slot = 0; slot < (4 * NM); ++slot)
-            e = __builtin_amdgcn_mfma_f64_16x16x4f64(xrow[16 * (slot >> 2) + (slot & 3)], x(slot), e, 0, 0, 0);
+            e = __builtin_amdgcn_mfma_f64_16x16x4f64(xrow[glm_eta_off(slot)], x(slot), e, 0, 0, 0);
         return e;
     };
     load_tile(0);
@@ -307,11 +308,11 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         constexpr int KM = 4 * NM;
         constexpr int kLA = 4;
         f64x4 eta_next = f64x4{0.0, 0.0, 0.0, 0.0};
-        const double* xrow1 = L.X + b1 * XS + p.cl * S + 4 * p.q;
-        const double* LY = L.Y + b * 16;
+        const double* xrow1 = L.X + b1 * XS + eta_lane;
+        const double* LY = L.X + b * XS + YO;
         double av[KM];
 #pragma unroll
-        for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow1[16 * (m >> 2) + (m & 3)];
+        for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow1[glm_eta_off(m)];
         double y[4], pr[4], term[4], rv[4];
         ExpTState E[4];
         LogTState Lg[4];
@@ -325,7 +326,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         for (int j = 0; j < NSUB; ++j) {
 #pragma unroll
             for (int m = j * KM / NSUB; m < (j + 1) * KM / NSUB; ++m) {
-                if (m + kLA < KM) av[m + kLA] = xrow1[16 * ((m + kLA) >> 2) + ((m + kLA) & 3)];
+                if (m + kLA < KM) av[m + kLA] = xrow1[glm_eta_off(m + kLA)];
                 eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x(m), eta_next, 0, 0, 0);
             }
             const int st = kGlmGroupRows ? j : j >> 2;
@@ -367,16 +368,16 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         if (GRAD) {
             // G tile T, k-slice kk: A[i][k] = X[obs 4kk+q][coord 16T+4(i&3)+(i>>2)], i = cl; kk outer so that
             // consecutive MFMAs feed independent accumulators; operands one kk ahead
-            const double* gcol = L.X + b * XS + 4 * (p.cl & 3) + (p.cl >> 2);
+            const double* gcol = L.X + b * XS + p.q * S + 4 * (p.cl & 3) + (p.cl >> 2);
             double ga[NM];
 #pragma unroll
-            for (int T = 0; T < NM; ++T) ga[T] = gcol[p.q * S + 16 * T];
+            for (int T = 0; T < NM; ++T) ga[T] = gcol[glm_g_off(T)];
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 double gn[NM];
                 if (kk < 3) {
 #pragma unroll
-                    for (int T = 0; T < NM; ++T) gn[T] = gcol[(4 * (kk + 1) + p.q) * S + 16 * T];
+                    for (int T = 0; T < NM; ++T) gn[T] = gcol[4 * (kk + 1) * S + glm_g_off(T)];
                 }
 #pragma unroll
                 for (int T = 0; T < NM; ++T) G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[T], rv[kk], G[T], 0, 0, 0);
@@ -403,16 +404,62 @@ __device__ __forceinline__ double glm_eval1(const GlmArgs& a, const GlmPos& p, c
     return glm_finish<NM, 1, GRAD>(a, p, L, x, G, lik_part, oos);
 }
 
+// LDS-DMA of staged tile tt into an LDS buffer: the image is contiguous (glm_layout.hpp), so each wave moves whole
+// 1-KiB pieces (global_load_lds_dwordx4: LDS M0 + 16 lane bytes), pieces w, w + 8, ... of the tile.  The copy is
+// counted on vmcnt only: the reader waits vmcnt(0) (glm_dma_wait) and passes a barrier after it (glm_eval).
+// Written as inline asm: the compiler's waitcnt pass treats a __builtin_amdgcn_global_load_lds as an LDS store
+// that may alias every later ds_write, and put an s_waitcnt vmcnt(0) before the eta-partial store right after the
+// eta MFMAs -- draining the next tile's copy a few hundred cycles after it was issued (r04 ISA).  The asm is
+// opaque to that pass; M0 has no other user in the regression kernels (checked in the ISA: every s_mov_b32 m0 is
+// one of these).  Loads the pass does track stay correctly waited for: vmcnt decrements in issue order, so an
+// extra load in flight only makes its counted waits longer.
+template <int TS>
+__device__ __forceinline__ void glm_dma_tile(const double* img, double* buf) {
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    constexpr int kPieces = TS / 128;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)buf;
+#pragma unroll
+    for (int j = 0; j < (kPieces + 7) / 8; ++j) {
+        const int c = w + 8 * j;
+        if (c < kPieces) {
+            const double* src = img + c * 128 + 2 * lane;
+            const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)c * 1024u));
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "s"(lds) : "memory");
+        }
+    }
+}
+// a workgroup barrier for LDS data written by ds_write (lgkmcnt) that leaves LDS-DMAs in flight: __syncthreads()
+// would also wait vmcnt(0), draining the next tile's copy (cdna_hip_programming.md §5, pipelining across barriers)
+__device__ __forceinline__ void glm_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void glm_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // log-target and (GRAD) gradient of the regression model at the lane's coordinates x.
 // Every wave of the workgroup calls it the same number of times (barriers inside).
 // gout doubles as the MFMA accumulator of G = X^T r (G[T] covers slots 4T..4T+3).
+//
+// d-sliced form (NW = 2, 4, 8 slices of DS = 16 NM = 128 coordinates; 8 / NW tiles of 16 chains per workgroup):
+// per 16-observation tile t, in LDS buffer t & 1 (one buffer at d_pad = 1024),
+//     LDS-DMA of tile t+1 into the other buffer (issued first, waited for at the end of the iteration)
+//     eta partial over the wave's slice (NM k-groups of MFMAs, operands read kLA ahead)  -> part[wave]
+//     barrier; the slice wave owning row r of its tile adds the NW partials left to right, the likelihood term and
+//     residual weight of that row -> rbuf[tile][r]
+//     barrier; every wave reads its tile's 4 rows' weights; G += X_t^T r (NM independent accumulators)
+//     vmcnt(0) + barrier: tile t+1 has landed and tile t's buffer, part and rbuf are free again.
+// Two tiles of chains share each staged tile (reuse 32 chains per X byte from L2 / MALL).
 template <int NM, int NW, bool GRAD>
 __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
                                         const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
     if constexpr (NW == 1) return glm_eval1<NM, GRAD>(a, p, L, XArr<4 * NM>{x}, G, oos);
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
-    const int S = g.lds_stride;
+    constexpr int DP = 16 * NM * NW;
+    constexpr int S = glm_row_stride(DP);
+    constexpr int XS = glm_tile_doubles(DP);
+    constexpr int YO = glm_y_offset(DP);
+    constexpr bool kOneBuf = DP > 512;                        // glm_xbufs: one LDS tile buffer
     const bool logistic = M.kind == MK_LOGISTIC;
     const double sgn = M.link_sign;
     const double sn = M.noise_sigma, s2n = sn * sn;
@@ -424,81 +471,64 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     }
     double lik_part = 0.0;
     const int64_t ntiles = g.n_pad / 16;
-    // X rows 16t..16t+15 (contiguous, 16 * d_pad doubles) are staged into padded LDS rows, double
-    // buffered: tile t+1's loads are issued before tile t's compute and written to the other buffer
-    // after it, so one barrier per tile retires both the readers of tile t and the writers of t+1.
-    constexpr int kBlk = glm_block<NW>();
-    constexpr int kHalf = 16 * 8 * NM * NW;                   // f64x2 per tile (d_pad = 16 NM NW)
-    constexpr int kPer = (kHalf + kBlk - 1) / kBlk;           // <= 8, 16 at d_pad = 1024 (one buffer)
-    constexpr bool kOneBuf = 16 * NM * NW > 512;              // glm_xbufs: one LDS tile buffer
-    constexpr int kLgHalfrow = __builtin_ctz(8 * NM * NW);
-    const int XS = 16 * S;                                    // doubles per LDS X buffer
-    f64x2 buf[kPer];
-    double ytile = 0.0;
-    auto load_tile = [&](int64_t tt) {
-        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * 16 * g.d_pad);
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = threadIdx.x + kBlk * j;
-            buf[j] = src[i < kHalf ? i : 0];                  // unconditional load: no exec branch
-        }
-        ytile = (threadIdx.x < 16) ? M.Y[tt * 16 + threadIdx.x] : 0.0;
-    };
-    auto store_tile = [&](int b) {
-        double* Xb = L.X + b * XS;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = threadIdx.x + kBlk * j;
-            if (i < kHalf) {
-                const int row = i >> kLgHalfrow, col = 2 * (i & ((1 << kLgHalfrow) - 1));
-                *reinterpret_cast<f64x2*>(&Xb[row * S + col]) = buf[j];
-            }
-        }
-        if (threadIdx.x < 16) L.Y[b * 16 + threadIdx.x] = ytile;
-    };
-    load_tile(0);
-    store_tile(0);
+    const int eta_lane = p.cl * S + 4 * p.q + p.base;                       // + glm_eta_off(slot)
+    const int g_lane = p.q * S + 4 * (p.cl & 3) + (p.cl >> 2) + p.base;   // + 4 kk S + glm_g_off(T)
+    glm_dma_tile<XS>(M.X, L.X);
+    glm_dma_wait();
     __syncthreads();
     for (int64_t t = 0; t < ntiles; ++t) {
         const int b = kOneBuf ? 0 : (int)(t & 1);
         const double* LX = L.X + b * XS;
-        const double* LY = L.Y + b * 16;
         const bool more = t + 1 < ntiles;
-        if (more && !kOneBuf) load_tile(t + 1);
-        // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e
-        f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
-        const double* xrow = LX + p.cl * S + p.base + 4 * p.q;
+        if (more && !kOneBuf) glm_dma_tile<XS>(M.X + (size_t)(t + 1) * XS, L.X + (b ^ 1) * XS);
+        // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e.  Every operand
+        // read is issued before the first MFMA (a scheduling fence keeps them there: left alone, the scheduler sank
+        // each read next to its MFMA and the chain waited out every LDS round trip); the waitcnt pass then waits
+        // for each MFMA's own read only.
+        constexpr int RPW = NW >= 4 ? 1 : 4 / NW;
+        const int r0 = p.slice * RPW;
+        const double* LY = LX + YO;
+        double yv[RPW];
 #pragma unroll
-        for (int slot = 0; slot < (4 * NM); ++slot) {
-            if (true) {
-                const double av = xrow[16 * (slot >> 2) + (slot & 3)];
-                eta = __builtin_amdgcn_mfma_f64_16x16x4f64(av, x[slot], eta, 0, 0, 0);
+        for (int rr_ = 0; rr_ < RPW; ++rr_) yv[rr_] = LY[p.q + 4 * ((r0 + rr_) & 3)];
+        f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
+        {
+            constexpr int KM = 4 * NM;
+            constexpr int kLA = NM <= 4 ? KM : 8;
+            const double* xrow = LX + eta_lane;
+            double av[KM];
+#pragma unroll
+            for (int m = 0; m < kLA; ++m) av[m] = xrow[glm_eta_off(m)];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < KM; ++m) {
+                if (m + kLA < KM) av[m + kLA] = xrow[glm_eta_off(m + kLA)];
+                eta = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x[m], eta, 0, 0, 0);
             }
         }
         // Elementwise part, split over the slice waves: wave slice s owns observation rows r in
-        // [s*RPW, (s+1)*RPW) of the tile (obs 16t + q + 4r for lane (q, cl)); with NW = 8 slices 4..7 own
-        // none.  Its eta is the slices' partials added left to right.
-        constexpr int RPW = NW >= 4 ? 1 : 4 / NW;
-        const int r0 = p.slice * RPW;
-        if (NW > 1) {
-            double* mine = L.part + (p.wave * 64 + p.lane) * 4;
-            mine[0] = eta[0]; mine[1] = eta[1]; mine[2] = eta[2]; mine[3] = eta[3];
-            __syncthreads();
+        // [s*RPW, (s+1)*RPW) of its tile (obs 16t + q + 4r for lane (q, cl)); with NW = 8 slices 4..7 own
+        // none.  Its eta is the slices' partials added left to right.  Partials are [wave][r][lane] (lane-contiguous
+        // 8-byte stores and loads: no bank conflicts), all NW of a row read before the first add.
+        {
+            double* mine = L.part + p.wave * 256 + p.lane;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mine[64 * r] = eta[r];
         }
+        glm_lds_barrier();
         double rv[4];
 #pragma unroll
         for (int rr_ = 0; rr_ < RPW; ++rr_) {
             const int r = r0 + rr_;
             if (r >= 4) break;
-            double e;
-            if (NW > 1) {
-                e = L.part[((p.tile * NW) * 64 + p.lane) * 4 + r];
-                for (int sl = 1; sl < NW; ++sl) e = e + L.part[((p.tile * NW + sl) * 64 + p.lane) * 4 + r];
-            } else {
-                e = eta[r];
-            }
+            double pe[NW];
+#pragma unroll
+            for (int sl = 0; sl < NW; ++sl) pe[sl] = L.part[(p.tile * NW + sl) * 256 + r * 64 + p.lane];
+            double e = pe[0];
+#pragma unroll
+            for (int sl = 1; sl < NW; ++sl) e = e + pe[sl];
             const int64_t obs = t * 16 + p.q + 4 * r;
-            const double y = LY[p.q + 4 * r];
+            const double y = yv[rr_];
             double term, w;
             if (logistic) {
                 const double tt = det_exp_tab(-(sgn * e));              // prob = 1/(1+exp(-X*vars))
@@ -513,42 +543,48 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             }
             const bool in = obs < M.n;
             if (in) lik_part = lik_part + term;
-            rv[(NW > 1) ? rr_ : r] = in ? w : 0.0;
+            rv[rr_] = in ? w : 0.0;
         }
-        if (NW > 1) {
+        // G tile T, k-slice kk': A[i][k] = X[obs 4kk'+q][coord base+16T+4(i&3)+(i>>2)], i = cl; kk outer so that
+        // consecutive MFMAs feed independent accumulators.  NM <= 4: all 4 NM operands are read before the weights
+        // barrier (they do not depend on it); NM = 8: one k-slice ahead.
+        constexpr int kGA = NM <= 4 ? 4 : 1;                      // k-slices of operands read up front
+        const double* gcol = LX + g_lane;
+        double ga[4][NM];
+        if (GRAD) {
+#pragma unroll
+            for (int kk = 0; kk < kGA; ++kk)
+#pragma unroll
+                for (int T = 0; T < NM; ++T) ga[kk][T] = gcol[4 * kk * S + glm_g_off(T)];
+        }
+        {
             // publish the owned rows' weights, then every slice wave reads all four for its G product
             double* rb = L.rbuf + p.tile * 256;
 #pragma unroll
             for (int rr_ = 0; rr_ < RPW; ++rr_)
                 if (r0 + rr_ < 4) rb[(r0 + rr_) * 64 + p.lane] = rv[rr_];
-            __syncthreads();
+            glm_lds_barrier();
 #pragma unroll
             for (int r = 0; r < 4; ++r) rv[r] = rb[r * 64 + p.lane];
         }
         if (GRAD) {
-            // G tile T, k-slice kk': A[i][k] = X[obs 4kk'+q][coord base+16T+4(i&3)+(i>>2)], i = cl
-            const double* gcol = LX + p.base + 4 * (p.cl & 3) + (p.cl >> 2);
 #pragma unroll
-            for (int T = 0; T < NM; ++T) {
-                if (true) {
+            for (int kk = 0; kk < 4; ++kk) {
+                if (kGA == 1 && kk < 3) {
 #pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const double av = gcol[(4 * kk + p.q) * S + 16 * T];
-                        G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, rv[kk], G[T], 0, 0, 0);
-                    }
+                    for (int T = 0; T < NM; ++T) ga[kk + 1][T] = gcol[4 * (kk + 1) * S + glm_g_off(T)];
                 }
+#pragma unroll
+                for (int T = 0; T < NM; ++T)
+                    G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[kk][T], rv[kk], G[T], 0, 0, 0);
             }
         }
         if (kOneBuf) {                                        // the one buffer: after its last reader of tile t
             __syncthreads();
-            if (more) {
-                load_tile(t + 1);
-                store_tile(0);
-            }
-        } else if (more) {
-            store_tile(b ^ 1);                                // the other buffer: its readers finished tile t-1
+            if (more) glm_dma_tile<XS>(M.X + (size_t)(t + 1) * XS, L.X);
         }
-        __syncthreads();
+        glm_dma_wait();                                       // tile t+1 landed (this wave's pieces) ...
+        __syncthreads();                                      // ... and every wave's; buffers, part, rbuf free
     }
     return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, lik_part, oos);
 }
@@ -1065,14 +1101,14 @@ __global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
 // work with its MFMAs.  Every sum is formed by the same instructions in the same order as glm_mala1 (eta chains
 // over (m, e, q); G chains over observations; a lane's likelihood terms in (t, r) order; qf / qb / prior as
 // there), so the results are glm_mala1's bit for bit and orc_glm_eval restates them.
-// LDS (doubles; XS = 16 lds_stride): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
+// LDS (doubles; XS = glm_tile_doubles(16 NM), X rows then Y): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
 // which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | tables | qf, lik [2][4][16].
 template <int NM>
 __host__ __device__ constexpr int glm_ws_region(int XS) {
     return (2 * XS + 4096) > (4 * 4 * NM * 64) ? (2 * XS + 4096) : (4 * 4 * NM * 64);
 }
-__host__ __device__ inline size_t glm_ws_lds_doubles(int nm, int lds_stride) {
-    const int XS = 16 * lds_stride;
+__host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
+    const int XS = glm_tile_doubles(16 * nm);
     const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
     return (size_t)(2 * XS + R + 4 * 16 + 4 * 128 + 2 * 64 + 2 * 4 * 16);
 }
@@ -1097,14 +1133,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     p.base = 0;
     p.c = ((int64_t)blockIdx.x * 4 + p.tile) * 16 + p.cl;
     p.live = p.c < s.C;
-    const int S = g.lds_stride;
-    const int XS = 16 * S;
+    constexpr int S = glm_row_stride(16 * NM);
+    constexpr int XS = glm_tile_doubles(16 * NM);             // one staged tile: X rows, then Y
+    constexpr int YO = glm_y_offset(16 * NM);
     double* const Xs = smem;                                   // 4 X tile slots: 0, 1 here, 2, 3 in region R
     double* const R = smem + 2 * XS;
     double* const Eb = R + 2 * XS;                             // eta [2][4 tiles][64 lanes][4]
     double* const Rb = Eb + 2048;                              // r   [2][4 tiles][64 lanes][4]
     double* const beta = R;                                    // proposal [4 tiles][NS][64] (proposal phase only)
-    double* const Yb = R + glm_ws_region<NM>(XS);              // Y [4][16]
+    double* const Yb = R + glm_ws_region<NM>(XS);              // (unused: Y travels inside each staged tile)
     double* const ltabp = Yb + 64;                             // logistic tables: log [128][4], exp [64][2]
     double* const qfl = ltabp + 4 * 128 + 2 * 64;              // qf [4][16], then lik [4][16]
     double* const likl = qfl + 64;
@@ -1123,32 +1160,26 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     const int64_t ntiles = g.n_pad / 16;
     const bool logi = M.kind == MK_LOGISTIC;
     // X / Y tile transfer, by the 256 threads of one wave role (u = thread index within the role)
-    constexpr int kHalf = 16 * 8 * NM;                         // f64x2 per tile (d_pad = 16 NM)
+    constexpr int kHalf = XS / 2;                              // f64x2 per staged tile
     constexpr int kPer = (kHalf + 255) / 256;
-    constexpr int kLgHalfrow = __builtin_ctz(8 * NM);
     const int u = (int)(threadIdx.x & 255);
     f64x2 xbuf[kPer];
-    double ybuf = 0.0;
-    auto load_tile = [&](int64_t tt) {
-        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * 16 * g.d_pad);
+    (void)Yb;
+    auto load_tile = [&](int64_t tt) {                         // the tile image moves linearly (glm_layout.hpp)
+        const f64x2* src = reinterpret_cast<const f64x2*>(M.X + (size_t)tt * XS);
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
             const int e = u + 256 * j;
             xbuf[j] = src[e < kHalf ? e : 0];
         }
-        ybuf = (u < 16) ? M.Y[tt * 16 + u] : 0.0;
     };
     auto store_tile = [&](int64_t tt) {
-        double* Xb = xslot(tt);
+        f64x2* dst = reinterpret_cast<f64x2*>(xslot(tt));
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
             const int e = u + 256 * j;
-            if (e < kHalf) {
-                const int row = e >> kLgHalfrow, col = 2 * (e & ((1 << kLgHalfrow) - 1));
-                *reinterpret_cast<f64x2*>(&Xb[row * S + col]) = xbuf[j];
-            }
+            if (e < kHalf) dst[e] = xbuf[j];
         }
-        if (u < 16) Yb[(tt & 3) * 16 + u] = ybuf;
     };
     double* const xb = beta + (size_t)(p.tile * NS) * 64 + p.lane;   // this lane's proposal slots
 
@@ -1210,27 +1241,27 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         constexpr int kLA = 4;
         double av[KM];
 #pragma unroll
-        for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow[16 * (m >> 2) + (m & 3)];
+        for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow[glm_eta_off(m)];
         f64x4 e = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
-            if (m + kLA < KM) av[m + kLA] = xrow[16 * ((m + kLA) >> 2) + ((m + kLA) & 3)];
+            if (m + kLA < KM) av[m + kLA] = xrow[glm_eta_off(m + kLA)];
             e = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bx[m], e, 0, 0, 0);
         }
         return e;
     };
     auto g_of = [&](int64_t tt) {                              // G += X_tt^T r_tt (glm_eval1_tiles' G product)
         const f64x4 rv = Rq[256 * (tt & 1)];
-        const double* gcol = xslot(tt) + 4 * (p.cl & 3) + (p.cl >> 2);
+        const double* gcol = xslot(tt) + p.q * S + 4 * (p.cl & 3) + (p.cl >> 2);
         double ga[NM];
 #pragma unroll
-        for (int T = 0; T < NM; ++T) ga[T] = gcol[p.q * S + 16 * T];
+        for (int T = 0; T < NM; ++T) ga[T] = gcol[glm_g_off(T)];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             double gn[NM];
             if (kk < 3) {
 #pragma unroll
-                for (int T = 0; T < NM; ++T) gn[T] = gcol[(4 * (kk + 1) + p.q) * S + 16 * T];
+                for (int T = 0; T < NM; ++T) gn[T] = gcol[4 * (kk + 1) * S + glm_g_off(T)];
             }
 #pragma unroll
             for (int T = 0; T < NM; ++T) G[T] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[T], rv[kk], G[T], 0, 0, 0);
@@ -1266,7 +1297,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                 if (t + 3 < ntiles) load_tile(t + 3);
             }
             const f64x4 eta = Eq[256 * (t & 1)];
-            const double* LY = Yb + (t & 3) * 16;
+            const double* LY = xslot(t) + YO;
             double y[4], pr[4], term[4], rv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
@@ -1593,7 +1624,7 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
     using namespace mcmc;
 #if GLM_MALA1_WS
     (void)lds;
-    const size_t lw = glm_ws_lds_doubles(a.g.nm, a.g.lds_stride) * sizeof(double);
+    const size_t lw = glm_ws_lds_doubles(a.g.nm) * sizeof(double);
     switch (nm) {
         case 1: glm_mala1ws<1><<<grid, 512, lw, st>>>(a); break;
         case 2: glm_mala1ws<2><<<grid, 512, lw, st>>>(a); break;
@@ -1616,29 +1647,46 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
 #else
 hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st);
 
+// 128 < d <= 512: d-slices of 64 coordinates (NM = 4; the default, which the oracle restates) or, with
+// MCMCHIP_GLM_SLICE=128 (a dev A/B switch for benches only), of 128 (NM = 8, two 16-chain tiles per workgroup:
+// that build spills the HMC / MALA state at the 256-register budget, r04 measurements in DESIGN.md §5.3)
+static bool glm_narrow_slices() {
+    static const bool v = [] {
+        const char* e = getenv("MCMCHIP_GLM_SLICE");
+        return !(e != nullptr && atoi(e) == 128);
+    }();
+    return v;
+}
+
 mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
-    // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1);
-    // 128 < d <= 512: NW = 4, 8 waves of DS = 64 (NM = 4) per tile, d_pad = 64 NW;
-    // 512 < d <= 1024: NW = 8 waves of DS = 128 (NM = 8), d_pad = 1024, one LDS tile buffer (glm_xbufs).
+    // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1), 4 tiles
+    // per workgroup;
+    // 128 < d <= 512: NW = d_pad / 64 slices (4 or 8) of DS = 64 coordinates (NM = 4), 8 / NW tiles of 16 chains
+    // per 8-wave workgroup (glm_narrow_slices);
+    // 512 < d <= 1024: NW = 8 slices of DS = 128 coordinates (NM = 8), one tile per workgroup; d_pad = 1024 keeps
+    // one LDS tile buffer (glm_xbufs).
     mcmc::GlmShape g{};
     if (d <= 128) {
         int nm = 1;
         while (16 * nm < d) nm *= 2;
         g.nw = 1;
         g.nm = nm;
-    } else if (d <= 512) {
-        int nw = 2;
+    } else if (d <= 512 && glm_narrow_slices()) {
+        int nw = 4;
         while (64 * nw < d) nw *= 2;
         g.nw = nw;
         g.nm = 4;
     } else {
-        g.nw = 8;
+        int nw = 2;
+        while (128 * nw < d) nw *= 2;
+        g.nw = nw;
         g.nm = 8;
     }
     g.ds = 16 * g.nm;
     g.d_pad = g.ds * g.nw;
-    g.tpw = (g.nw > 4 ? g.nw : 4) / g.nw;
-    g.lds_stride = g.d_pad + 2;
+    g.tpw = g.nw == 1 ? 4 : 8 / g.nw;
+    g.lds_stride = mcmc::glm_row_stride(g.d_pad);
+    g.ts = mcmc::glm_tile_doubles(g.d_pad);
     g.n_pad = (n + 15) / 16 * 16;
     return g;
 }
@@ -1653,6 +1701,26 @@ int mcmc_glm_steps_per_launch(int d, int64_t n, int sampler_kind) {
 }
 
 int mcmc_glm_d_pad(int d) { return mcmc_glm_shape(d, 1).d_pad; }
+
+size_t mcmc_glm_image_doubles(int d, int64_t n) {
+    const mcmc::GlmShape g = mcmc_glm_shape(d, n);
+    return (size_t)(g.n_pad / 16) * (size_t)g.ts;
+}
+
+// the staged-tile image of X [n][d] (row-major) and Y [n] (glm_layout.hpp): tile t = rows 16t..16t+15 at
+// positions glm_pos(k) of stride S, then Y; zeros elsewhere (padded rows, coordinates k >= d, gaps)
+void mcmc_glm_pack_image(int d, int64_t n, const double* X, const double* Y, double* img) {
+    const mcmc::GlmShape g = mcmc_glm_shape(d, n);
+    const size_t total = mcmc_glm_image_doubles(d, n);
+    for (size_t i = 0; i < total; ++i) img[i] = 0.0;
+    const int S = g.lds_stride, YO = mcmc::glm_y_offset(g.d_pad);
+    for (int64_t i = 0; i < n; ++i) {
+        double* tile = img + (size_t)(i / 16) * (size_t)g.ts;
+        const int r = (int)(i % 16);
+        for (int k = 0; k < d; ++k) tile[r * S + k] = X[(size_t)i * d + k];
+        tile[YO + r] = Y[i];
+    }
+}
 
 template <int NM, int NW>
 static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
@@ -1701,6 +1769,8 @@ hipError_t mcmc_launch_glm_step(const mcmc::KernelArgs& k, hipStream_t st) {
         case 81: return glm_step_nm<8, 1>(a, lds, grid, st);
         case 44: return glm_step_nm<4, 4>(a, lds, grid, st);
         case 48: return glm_step_nm<4, 8>(a, lds, grid, st);
+        case 82: return glm_step_nm<8, 2>(a, lds, grid, st);
+        case 84: return glm_step_nm<8, 4>(a, lds, grid, st);
         case 88: return glm_step_nm<8, 8>(a, lds, grid, st);
         default: return hipErrorInvalidValue;
     }
@@ -1730,6 +1800,8 @@ hipError_t mcmc_launch_glm_record(const mcmc::KernelArgs& k, const mcmc::LeapRec
         case 81: return glm_rec_nm<8, 1>(a, lds, grid, st);
         case 44: return glm_rec_nm<4, 4>(a, lds, grid, st);
         case 48: return glm_rec_nm<4, 8>(a, lds, grid, st);
+        case 82: return glm_rec_nm<8, 2>(a, lds, grid, st);
+        case 84: return glm_rec_nm<8, 4>(a, lds, grid, st);
         case 88: return glm_rec_nm<8, 8>(a, lds, grid, st);
         default: return hipErrorInvalidValue;
     }
@@ -1749,6 +1821,8 @@ hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& k, const double* xin, do
         case 81: glm_eval_kernel<8, 1><<<grid, glm_block<1>(), lds, st>>>(a, xin, lp, g, check); break;
         case 44: glm_eval_kernel<4, 4><<<grid, glm_block<4>(), lds, st>>>(a, xin, lp, g, check); break;
         case 48: glm_eval_kernel<4, 8><<<grid, glm_block<8>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 82: glm_eval_kernel<8, 2><<<grid, glm_block<2>(), lds, st>>>(a, xin, lp, g, check); break;
+        case 84: glm_eval_kernel<8, 4><<<grid, glm_block<4>(), lds, st>>>(a, xin, lp, g, check); break;
         case 88: glm_eval_kernel<8, 8><<<grid, glm_block<8>(), lds, st>>>(a, xin, lp, g, check); break;
         default: return hipErrorInvalidValue;
     }

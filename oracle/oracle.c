@@ -176,9 +176,9 @@ static double orc_sum(const double* t, const orc_model* mdl, int order) {
 
 /* ------------------------------------------------------------ regression models (MFMA kernels) */
 /* Geometry of the regression kernels (glm.hip mcmc_glm_shape): d <= 128: one wave per 16-chain tile with
-   DS = d_pad = 16 NM (NM a power of two); 128 < d <= 512: NW = 4, 8 waves of DS = 64 coordinates,
-   d_pad = 64 NW; 512 < d <= 1024: NW = 8 waves of DS = 128, d_pad = 1024; n_pad = round_up(n,16).  Lane quarter q of the wave for slice s owns coordinates
-   k = s*DS + 16m + 4q + e (m < DS/16, e < 4). */
+   DS = d_pad = 16 NM (NM a power of two); 128 < d <= 512: NW = 4 or 8 d-slices of DS = 64 coordinates (NM = 4),
+   d_pad = 64 NW; 512 < d <= 1024: NW = 8 d-slices of DS = 128 (NM = 8), d_pad = 1024; n_pad = round_up(n,16).
+   Lane quarter q of the wave for slice s owns coordinates k = s*DS + 16m + 4q + e (m < DS/16, e < 4). */
 static orc_glm_geo orc_glm_geometry(const orc_model* m) {
     orc_glm_geo g;
     int nm = 1, nw = 1;
