@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "bm_log_table.inc"
+#include "erfc_table.inc"
 
 namespace mcmc {
 
@@ -586,6 +587,61 @@ __device__ __forceinline__ double round_away(double x) {
     if (fr >= 0.5) t += 1.0;
     else if (fr <= -0.5) t -= 1.0;
     return t;
+}
+
+// erfc, erfcx, log1p and the normal log-cdf of the probit model (examples/probit_regression.jl:26-30): the oracle's
+// orc_erfcx_ge_half / orc_erfc / orc_log1p / orc_normlogcdf operation for operation (scripts/gen_erfc_table.py;
+// DESIGN.md §3).
+static __device__ const double kErfcTaylor[14] = {ERFC_TAYLOR_COEFS};
+static __device__ const double kErfcPoly[32][13] = {ERFC_POLY_ROWS};
+__device__ __forceinline__ double det_erfcx_ge_half(double x) {     // x >= 1/2
+    if (x >= 128.0) {
+        const double v = 1.0 / (x * x);
+        const double s = __builtin_fma(__builtin_fma(__builtin_fma(v, -1.875, 0.75), v, -0.5), v, 1.0);
+        return s / (x * 0x1.c5bf891b4ef6bp+0);
+    }
+    const uint64_t bx = d2bits(x);
+    const uint32_t hx = (uint32_t)(bx >> 32);
+    const int i = (int)(hx >> 18) - (1022 << 2);                   // binade quarter, 0..31
+    const double c = bits2d((uint64_t)((hx & 0xfffc0000u) | 0x00020000u) << 32);
+    const double sc = bits2d((uint64_t)(2046u - (hx >> 20) + 3u) << 52);   // 2^(3-e)
+    const double t = (x - c) * sc;                                  // exact, in [-1, 1]
+    const double* P = kErfcPoly[i];
+    double p = P[12];
+#pragma unroll
+    for (int n = 11; n >= 0; --n) p = __builtin_fma(p, t, P[n]);
+    return p;
+}
+__device__ __forceinline__ double det_erfc(double a) {
+    const double x = __builtin_fabs(a);
+    double r;
+    if (x < 0.5) {
+        const double u = x * x;
+        double q = kErfcTaylor[13];
+#pragma unroll
+        for (int n = 12; n >= 0; --n) q = __builtin_fma(q, u, kErfcTaylor[n]);
+        r = 1.0 - x * q;
+    } else if (x < 32.0) {
+        const double p = det_erfcx_ge_half(x);
+        const double xh = bits2d(d2bits(x) & 0xfffffffff8000000ull);   // 26 significant bits: xh * xh exact
+        const double e1 = det_exp(-(xh * xh));
+        const double e2 = det_exp(-((x - xh) * (x + xh)));
+        r = (e1 * e2) * p;
+    } else {
+        r = 0.0;
+    }
+    r = a < 0.0 ? 2.0 - r : r;
+    return a != a ? a : r;
+}
+__device__ __forceinline__ double det_log1p(double t) {
+    const double u = 1.0 + t;
+    return u == 1.0 ? t : det_log(u) * (t / (u - 1.0));
+}
+__device__ __forceinline__ double det_normlogcdf(double z) {
+    const double invsqrt2 = 0x1.6a09e667f3bcdp-1;
+    const double r = z < -1.0 ? det_log(det_erfcx_ge_half(-z * invsqrt2) / 2.0) - (z * z) / 2.0
+                              : det_log1p(-det_erfc(z * invsqrt2) / 2.0);
+    return z != z ? z : r;
 }
 
 }  // namespace mcmc

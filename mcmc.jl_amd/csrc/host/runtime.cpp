@@ -372,6 +372,7 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
             break;
         }
         case MCMC_MODEL_LOGISTIC:
+        case MCMC_MODEL_PROBIT:
         case MCMC_MODEL_LINEAR: {
             if (d > mcmc_glm_max_d()) return bail(fail(MCMC_E_UNSUPPORTED, "regression models support d <= 1024"));
             if (desc->n <= 0 || !desc->X || !desc->Y) return bail(fail(MCMC_E_INVALID_ARG, "regression needs n > 0, X, Y"));
@@ -380,10 +381,12 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
                 return bail(fail(MCMC_E_INVALID_ARG, "noise sigma should be > 0"));
             if (desc->kind == MCMC_MODEL_LOGISTIC && !(desc->link_sign == 1.0 || desc->link_sign == -1.0))
                 return bail(fail(MCMC_E_INVALID_ARG, "link_sign must be +1 or -1"));
-            if (desc->kind == MCMC_MODEL_LOGISTIC)
+            if (desc->kind == MCMC_MODEL_LOGISTIC || desc->kind == MCMC_MODEL_PROBIT)
                 for (int64_t i = 0; i < desc->n; ++i)
                     if (!(desc->Y[i] == 0.0 || desc->Y[i] == 1.0))
-                        return bail(fail(MCMC_E_INVALID_ARG, "logistic responses must be 0 or 1 (Bernoulli)"));
+                        return bail(fail(MCMC_E_INVALID_ARG, desc->kind == MCMC_MODEL_LOGISTIC
+                                                                 ? "logistic responses must be 0 or 1 (Bernoulli)"
+                                                                 : "probit responses must be 0 or 1"));
             // the kernels' staged-tile image of X and Y (glm_layout.hpp: 16-row tiles in the LDS layout, Y inside
             // each tile, zero padding), plus Y [n_pad] on its own
             const int64_t n_pad = (desc->n + 15) / 16 * 16;
@@ -442,7 +445,9 @@ static bool model_is_separable(const mcmc_model* m) {
     return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL || m->args.kind == MK_ABS_NORMAL ||
            m->args.kind == MK_DIST;
 }
-static bool model_is_glm(const mcmc_model* m) { return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR; }
+static bool model_is_glm(const mcmc_model* m) {
+    return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR || m->args.kind == MK_PROBIT;
+}
 
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 

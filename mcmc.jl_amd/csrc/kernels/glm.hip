@@ -38,6 +38,9 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <int NW>
 constexpr int glm_block() { return NW == 1 ? 256 : 512; }
 constexpr int kGlmMaxWaves = 8;
+#ifdef GLM_STAMP
+constexpr int kGlmStampLdsBytes = 8 * 16 * 8 * 4;     // GLM_STAMP builds: the phase stamps' LDS (glm_eval)
+#endif
 // glm_eval1's elementwise schedule (the same operations either way): each sub-stage between
 // eta MFMAs runs one stage of one observation row (0) or of all four rows of the lane (1)
 #ifndef GLM_GROUP_ROWS
@@ -141,7 +144,11 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
 
 static size_t glm_lds_bytes(const GlmShape& g) {
     return (size_t)(glm_xbufs(g.nw, g.d_pad) * g.ts + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
-                    4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8;
+                    4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8
+#ifdef GLM_STAMP
+           + 16 + (g.nw > 1 ? kGlmStampLdsBytes : 0)
+#endif
+        ;
 }
 
 // sum of a per-chain quantity held as 4 quarter partials per wave and NW slice partials:
@@ -217,6 +224,16 @@ __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, 
     return acc;
 }
 
+// The probit model's elementwise part for one observation (examples/probit_regression.jl:26-40; oracle orc_glm_eval):
+// term = y logcdf(N, eta) + (1 - y) logcdf(N, -eta), and its eta-derivative, the example's grad_log_posterior weight
+// y exp(A - logcdf(N, eta)) - (1 - y) exp(A - logcdf(N, -eta)), A = -(eta^2 + log(2 pi))/2
+__device__ __forceinline__ void glm_probit_obs(double eta, double y, double& term, double& w) {
+    const double la = det_normlogcdf(eta), lb = det_normlogcdf(-eta);
+    term = y * la + (1.0 - y) * lb;
+    const double A = (-(eta * eta + kLog2Pi)) / 2.0;
+    w = y * det_exp(A - la) - (1.0 - y) * det_exp(A - lb);
+}
+
 // Single-slice evaluation (NW = 1: the wave holds all d_pad coordinates of its 16 chains), software
 // pipelined over the 16-observation tiles with three LDS tile buffers:
 //     iteration t:  eta_{t+1} = X_{t+1} beta   (MFMA chain, buffer (t+1) % 3)
@@ -233,6 +250,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
     const GlmShape& g = a.g;
     constexpr int S = glm_row_stride(16 * NM);
     const double sgn = M.link_sign;
+    const bool probit = !LOGI && M.kind == MK_PROBIT;          // probit runs in the linear instantiation (uniform)
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = LOGI ? 0.0 : det_log(sn);
     const double isn = 1.0 / sn, is2n = 1.0 / s2n;
@@ -345,6 +363,8 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
                             rv[r] = sgn * (y[r] - pr[r]);                           // MCMCDerivRules.jl:111, closed form
                             break;
                     }
+                } else if (probit) {
+                    glm_probit_obs(eta[r], y[r], term[r], rv[r]);
                 } else {
                     const double resid = y[r] - eta[r];                             // resid = Y - X*vars
                     const double z = resid * isn;
@@ -414,27 +434,54 @@ __device__ __forceinline__ double glm_eval1(const GlmArgs& a, const GlmPos& p, c
 // one of these).  Loads the pass does track stay correctly waited for: vmcnt decrements in issue order, so an
 // extra load in flight only makes its counted waits longer.
 template <int TS>
-__device__ __forceinline__ void glm_dma_tile(const double* img, double* buf) {
+constexpr int glm_dma_pieces_per_wave() { return (TS / 128 + 7) / 8; }
+// piece j (0 <= j < glm_dma_pieces_per_wave) of this wave's share of tile image img -> LDS buffer buf
+template <int TS>
+__device__ __forceinline__ void glm_dma_piece(const double* img, double* buf, int j) {
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     constexpr int kPieces = TS / 128;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)buf;
-#pragma unroll
-    for (int j = 0; j < (kPieces + 7) / 8; ++j) {
-        const int c = w + 8 * j;
-        if (c < kPieces) {
-            const double* src = img + c * 128 + 2 * lane;
-            const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)c * 1024u));
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "s"(lds) : "memory");
-        }
+    const int c = w + 8 * j;
+    if (c < kPieces) {
+        const double* src = img + c * 128 + 2 * lane;
+        const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(uintptr_t)buf + (uint32_t)c * 1024u));
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "s"(lds) : "memory");
     }
 }
+template <int TS>
+__device__ __forceinline__ void glm_dma_tile(const double* img, double* buf) {
+#pragma unroll
+    for (int j = 0; j < glm_dma_pieces_per_wave<TS>(); ++j) glm_dma_piece<TS>(img, buf, j);
+}
+// GLM_DMA_SPREAD (default 0): the next tile's pieces issued between the eta MFMAs (one after every second MFMA)
+// instead of all before the eta operand reads
+#ifndef GLM_DMA_SPREAD
+#define GLM_DMA_SPREAD 0
+#endif
 // a workgroup barrier for LDS data written by ds_write (lgkmcnt) that leaves LDS-DMAs in flight: __syncthreads()
 // would also wait vmcnt(0), draining the next tile's copy (cdna_hip_programming.md §5, pipelining across barriers)
 __device__ __forceinline__ void glm_lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 __device__ __forceinline__ void glm_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// GLM_STAMP (dev build only, scripts/glm_stamps.py): shader-clock stamps (low 32 bits) of the d-sliced tile loop's
+// phases, every wave of workgroups 0..3, tiles 8..23 of the last evaluation (the points: loop top, eta partial
+// stored, barrier 1, weights stored, barrier 2, G issued, tile t+1 landed, barrier 3).  They are kept in 4 KB of LDS
+// past the kernel's own (global stores inside the loop would count on vmcnt and stretch the DMA wait they measure)
+// and copied out after the loop.
+#ifdef GLM_STAMP
+static __device__ unsigned g_glm_stamps[4][8][16][8];
+#define GLM_STAMPT(pt)                                                                                  \
+    do {                                                                                               \
+        if (t >= 8 && t < 24) {                                                                        \
+            const unsigned ts_ = (unsigned)__builtin_amdgcn_s_memtime();                              \
+            if ((threadIdx.x & 63) == 0) stamp_lds[((threadIdx.x >> 6) * 16 + (t - 8)) * 8 + (pt)] = ts_; \
+        }                                                                                              \
+    } while (0)
+#else
+#define GLM_STAMPT(pt) do { } while (0)
+#endif
 
 // log-target and (GRAD) gradient of the regression model at the lane's coordinates x.
 // Every wave of the workgroup calls it the same number of times (barriers inside).
@@ -473,14 +520,20 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     const int64_t ntiles = g.n_pad / 16;
     const int eta_lane = p.cl * S + 4 * p.q + p.base;                       // + glm_eta_off(slot)
     const int g_lane = p.q * S + 4 * (p.cl & 3) + (p.cl >> 2) + p.base;   // + 4 kk S + glm_g_off(T)
+#ifdef GLM_STAMP
+    unsigned* const stamp_lds = reinterpret_cast<unsigned*>(L.iscr + 4);
+#endif
     glm_dma_tile<XS>(M.X, L.X);
     glm_dma_wait();
     __syncthreads();
     for (int64_t t = 0; t < ntiles; ++t) {
+        GLM_STAMPT(0);
         const int b = kOneBuf ? 0 : (int)(t & 1);
         const double* LX = L.X + b * XS;
         const bool more = t + 1 < ntiles;
-        if (more && !kOneBuf) glm_dma_tile<XS>(M.X + (size_t)(t + 1) * XS, L.X + (b ^ 1) * XS);
+        const double* const nimg = M.X + (size_t)(t + 1) * XS;
+        double* const nbuf = L.X + (b ^ 1) * XS;
+        if (!GLM_DMA_SPREAD && more && !kOneBuf) glm_dma_tile<XS>(nimg, nbuf);
         // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e.  Every operand
         // read is issued before the first MFMA (a scheduling fence keeps them there: left alone, the scheduler sank
         // each read next to its MFMA and the chain waited out every LDS round trip); the waitcnt pass then waits
@@ -504,6 +557,14 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             for (int m = 0; m < KM; ++m) {
                 if (m + kLA < KM) av[m + kLA] = xrow[glm_eta_off(m + kLA)];
                 eta = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x[m], eta, 0, 0, 0);
+                if (GLM_DMA_SPREAD && !kOneBuf && (m & 1) && (m >> 1) < glm_dma_pieces_per_wave<XS>()) {
+                    if (more) glm_dma_piece<XS>(nimg, nbuf, m >> 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (GLM_DMA_SPREAD && !kOneBuf && more) {
+#pragma unroll
+                for (int j = KM / 2; j < glm_dma_pieces_per_wave<XS>(); ++j) glm_dma_piece<XS>(nimg, nbuf, j);
             }
         }
         // Elementwise part, split over the slice waves: wave slice s owns observation rows r in
@@ -515,7 +576,9 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
 #pragma unroll
             for (int r = 0; r < 4; ++r) mine[64 * r] = eta[r];
         }
+        GLM_STAMPT(1);
         glm_lds_barrier();
+        GLM_STAMPT(2);
         double rv[4];
 #pragma unroll
         for (int rr_ = 0; rr_ < RPW; ++rr_) {
@@ -535,6 +598,8 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
                 const double pr = 1.0 / (1.0 + tt);
                 term = det_log_tab((y >= 0.5) ? pr : 1.0 - pr);         // Y ~ Bernoulli(prob)
                 w = sgn * (y - pr);                                     // MCMCDerivRules.jl:111 chain, closed form
+            } else if (M.kind == MK_PROBIT) {
+                glm_probit_obs(e, y, term, w);
             } else {
                 const double resid = y - e;                             // resid = Y - X*vars
                 const double z = resid * isn;
@@ -563,7 +628,9 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
 #pragma unroll
             for (int rr_ = 0; rr_ < RPW; ++rr_)
                 if (r0 + rr_ < 4) rb[(r0 + rr_) * 64 + p.lane] = rv[rr_];
+            GLM_STAMPT(3);
             glm_lds_barrier();
+            GLM_STAMPT(4);
 #pragma unroll
             for (int r = 0; r < 4; ++r) rv[r] = rb[r * 64 + p.lane];
         }
@@ -583,9 +650,16 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             __syncthreads();
             if (more) glm_dma_tile<XS>(M.X + (size_t)(t + 1) * XS, L.X);
         }
+        GLM_STAMPT(5);
         glm_dma_wait();                                       // tile t+1 landed (this wave's pieces) ...
+        GLM_STAMPT(6);
         __syncthreads();                                      // ... and every wave's; buffers, part, rbuf free
+        GLM_STAMPT(7);
     }
+#ifdef GLM_STAMP
+    if (blockIdx.x < 4 && (threadIdx.x & 63) == 0)
+        for (int j = 0; j < 16 * 8; ++j) (&g_glm_stamps[blockIdx.x][threadIdx.x >> 6][0][0])[j] = stamp_lds[(threadIdx.x >> 6) * 128 + j];
+#endif
     return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, lik_part, oos);
 }
 
@@ -1319,6 +1393,9 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                     term[r] = det_log_tab_fin(Lg[r]);
                     rv[r] = sgn * (y[r] - pr[r]);                                  // MCMCDerivRules.jl:111, closed form
                 }
+            } else if (M.kind == MK_PROBIT) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) glm_probit_obs(eta[r], y[r], term[r], rv[r]);
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -1828,4 +1905,9 @@ hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& k, const double* xin, do
     }
     return hipGetLastError();
 }
+#ifdef GLM_STAMP
+extern "C" int mcmc_debug_glm_stamps(long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcmc::g_glm_stamps), sizeof(mcmc::g_glm_stamps)) == hipSuccess ? 0 : 4;
+}
+#endif
 #endif  // GLM_MALA1_UNIT

@@ -89,9 +89,25 @@ __global__ void k_detmath(int op, int64_t n, const double* x, const double* y, d
         case 15: r = gt_det_log(a, y[i]) ? 1.0 : 0.0; break;      // the screened accept test: a > det_log(y)
         case 16: r = bm_rad2_u32((uint32_t)(uint64_t)a); break;    // the Box-Muller radius^2, -2 log u
         case 17: r = bm_radius_u32((uint32_t)(uint64_t)a, rad_tab_global()); break;   // the radius polynomial
+        case 18: r = det_erfc(a); break;                           // probit model: erfc, log1p, normal log-cdf
+        case 19: r = det_log1p(a); break;
+        case 20: r = det_normlogcdf(a); break;
         default: r = 0.0;
     }
     out[i] = r;
+}
+
+// op 21: bm_radius_u32 reading its coefficients from an LDS copy of the table, as the hot kernels do (samplers.hpp
+// kTabLds).  Tail lanes (v < 2^21, including v = 0) form an out-of-range LDS row address there and discard what it
+// reads (detmath.hpp bm_radius_u32, RadTab.lds): this kernel drives those inputs so the tests see the LDS path give
+// the global path's values (the hardware returns 0 for an LDS read outside the allocation, MI355X ISA).
+__global__ void k_radius_lds(int64_t n, const double* x, double* out) {
+    extern __shared__ __attribute__((aligned(16))) double tab[];
+    for (int j = threadIdx.x; j < 4 * BM_RADP_NROWS * 2; j += blockDim.x) tab[j] = (&kBmRadPTab[0][0])[j];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = bm_radius_u32((uint32_t)(uint64_t)x[i], RadTab{reinterpret_cast<const double (*)[2]>(tab), true});
 }
 
 __global__ void k_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
@@ -162,7 +178,10 @@ hipError_t mcmc_transpose(double* dst, int64_t ldd, const double* src, int64_t l
     return hipSuccess;
 }
 hipError_t mcmc_detmath(int op, int64_t n, const double* x, const double* y, double* out, hipStream_t st) {
-    mcmc::k_detmath<<<nblk(n, 256), 256, 0, st>>>(op, n, x, y, out);
+    if (op == 21)
+        mcmc::k_radius_lds<<<nblk(n, 256), 256, 4 * BM_RADP_NROWS * 2 * sizeof(double), st>>>(n, x, out);
+    else
+        mcmc::k_detmath<<<nblk(n, 256), 256, 0, st>>>(op, n, x, y, out);
     return hipGetLastError();
 }
 hipError_t mcmc_philox(int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out, hipStream_t st) {

@@ -30,7 +30,7 @@ from . import _lib
 from ._lib import check, dptr
 
 __all__ = [
-    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "LogisticRegression", "LinearRegression", "MCMCLikelihoodModel", "model",
+    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "LogisticRegression", "LinearRegression", "ProbitRegression", "vaso_data", "MCMCLikelihoodModel", "model",
     "RWM", "MALA", "HMC", "HMCDA", "RAM", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
     "run", "resume", "device_count",
 ]
@@ -124,6 +124,29 @@ class LinearRegression:
         self.X = np.ascontiguousarray(np.asarray(X, dtype=np.float64))
         self.Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
         self.prior_sigma, self.noise_sigma = float(prior_sigma), float(noise_sigma)
+
+
+class ProbitRegression:
+    """examples/probit_regression.jl:18-40: log-prior MvNormal(zeros(d), prior_sigma^2 I) (priorstd = 10 in the
+    example) + dot(logcdf(Normal(), X*pars), Y) + dot(logcdf(Normal(), -X*pars), 1 - Y), Y in {0, 1}; gradient
+    X'*(Y.*exp(A - logcdf(X*pars)) - (1 - Y).*exp(A - logcdf(-X*pars))) - pars/prior_sigma^2, A = -((X*pars).^2 +
+    log(2pi))/2.  vaso_data() builds the example's design matrix."""
+    kind = _lib.MODEL_PROBIT
+
+    def __init__(self, X, Y, prior_sigma: float = 10.0):
+        self.X = np.ascontiguousarray(np.asarray(X, dtype=np.float64))
+        self.Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
+        self.prior_sigma = float(prior_sigma)
+
+
+def vaso_data(path):
+    """The probit example's design matrix (examples/probit_regression.jl:7-16): vaso.txt's covariates standardised
+    (mean / sample std per column), polynomial order 1, a leading column of ones; the last column is y."""
+    vaso = np.loadtxt(path)
+    cov, y = vaso[:, :-1], vaso[:, -1]
+    cov = (cov - cov.mean(axis=0)) / cov.std(axis=0, ddof=1)
+    X = np.hstack([np.ones((cov.shape[0], 1)), cov])
+    return X, y
 
 
 class MCMCLikelihoodModel:

@@ -31,6 +31,7 @@
 #include <math.h>
 
 #include "bm_log_table.inc"
+#include "erfc_table.inc"
 
 #define ORC_PHILOX_M0 0xD2511F53u
 #define ORC_PHILOX_M1 0xCD9E8D57u
@@ -362,6 +363,71 @@ static inline double orc_round_away(double x) {
     if (fr >= 0.5) t += 1.0;
     else if (fr <= -0.5) t -= 1.0;
     return t;
+}
+
+/* ------------------------------------------------------- erfc, erfcx and the normal log-cdf (probit model) */
+/* erfcx(x) = exp(x^2) erfc(x) for x >= 1/2 (scripts/gen_erfc_table.py): x < 128: P_i(t) on the binade quarter i
+   (i = (biased exponent, top two mantissa bits) - (1022 << 2), t = (x - c) 2^(3-e) exact); x >= 128: the asymptotic
+   series 1/(x sqrt(pi)) (1 - 1/(2x^2) + 3/(4x^4) - 15/(8x^6)).
+   erfc(x): |x| < 1/2: 1 - x Q(x^2) (Taylor); |x| < 32: exp(-x^2) erfcx(|x|), exp(-x^2) = exp(-xh^2) exp(-(x - xh)
+   (x + xh)) with xh = x to 26 bits (xh^2 exact); beyond: 0; negative x: 2 - erfc(-x).  Device twins: det_erfcx,
+   det_erfc (detmath.hpp), operation for operation. */
+static const double orc_erfc_taylor[14] = {ERFC_TAYLOR_COEFS};
+static const double orc_erfc_poly[32][13] = {ERFC_POLY_ROWS};
+static inline double orc_erfcx_ge_half(double x) {
+    if (x >= 128.0) {
+        const double v = 1.0 / (x * x);
+        const double s = fma(fma(fma(v, -1.875, 0.75), v, -0.5), v, 1.0);
+        return s / (x * 0x1.c5bf891b4ef6bp+0);                     /* x sqrt(pi) */
+    }
+    const uint64_t bx = orc_d2bits(x);
+    const uint32_t hx = (uint32_t)(bx >> 32);
+    const int i = (int)(hx >> 18) - (1022 << 2);                   /* binade quarter, 0..31 */
+    const double c = orc_bits2d((uint64_t)((hx & 0xfffc0000u) | 0x00020000u) << 32);
+    const double sc = orc_bits2d((uint64_t)(2046u - (hx >> 20) + 3u) << 52);   /* 2^(3-e) */
+    const double t = (x - c) * sc;                                 /* exact, in [-1, 1] */
+    const double* P = orc_erfc_poly[i];
+    double p = P[12];
+    for (int n = 11; n >= 0; --n) p = fma(p, t, P[n]);
+    return p;
+}
+static inline double orc_erfc(double a) {
+    if (a != a) return a;
+    const double x = fabs(a);
+    double r;
+    if (x < 0.5) {
+        const double u = x * x;
+        double q = orc_erfc_taylor[13];
+        for (int n = 12; n >= 0; --n) q = fma(q, u, orc_erfc_taylor[n]);
+        r = 1.0 - x * q;
+    } else if (x < 32.0) {
+        const double p = orc_erfcx_ge_half(x);
+        const double xh = orc_bits2d(orc_d2bits(x) & 0xfffffffff8000000ull);   /* 26 significant bits */
+        const double e1 = orc_exp(-(xh * xh));
+        const double e2 = orc_exp(-((x - xh) * (x + xh)));
+        r = (e1 * e2) * p;
+    } else {
+        r = 0.0;
+    }
+    return a < 0.0 ? 2.0 - r : r;
+}
+
+/* log1p(t) for t > -1: u = 1 + t; t when u == 1, else log(u) t / (u - 1) (Goldberg, What Every Computer Scientist
+   ..., theorem 4: a few ulp with a faithful log) */
+static inline double orc_log1p(double t) {
+    const double u = 1.0 + t;
+    if (u == 1.0) return t;
+    return orc_log(u) * (t / (u - 1.0));
+}
+
+/* logcdf(Normal(), z) in StatsFuns.jl's form (normlogcdf; Distributions.jl, an unpinned REQUIRE dependency of the
+   reference, absent here): z < -1: log(erfcx(-z/sqrt2)/2) - z^2/2 (finite down to -Inf: no erfc underflow);
+   else log1p(-erfc(z/sqrt2)/2); 1/sqrt2 as a multiplication */
+static inline double orc_normlogcdf(double z) {
+    const double invsqrt2 = 0x1.6a09e667f3bcdp-1;
+    if (z != z) return z;
+    if (z < -1.0) return orc_log(orc_erfcx_ge_half(-z * invsqrt2) / 2.0) - (z * z) / 2.0;
+    return orc_log1p(-orc_erfc(z * invsqrt2) / 2.0);
 }
 
 #endif

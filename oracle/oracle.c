@@ -33,6 +33,7 @@
 #define ORC_MODEL_LINEAR 4
 #define ORC_MODEL_ABS_NORMAL 5
 #define ORC_MODEL_DIST 6
+#define ORC_MODEL_PROBIT 7
 
 #define ORC_RWM 1
 #define ORC_MALA 2
@@ -100,7 +101,9 @@ typedef struct { int d_pad, nw, ds; int64_t n_pad; } orc_glm_geo;
 static orc_glm_geo orc_glm_geometry(const orc_model* m);
 static double orc_glm_sum(const double* t, const orc_glm_geo* g, int d, int fused_sq);
 
-static int orc_is_glm(const orc_model* m) { return m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR; }
+static int orc_is_glm(const orc_model* m) {
+    return m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR || m->kind == ORC_MODEL_PROBIT;
+}
 
 /* order ORC_ORDER_PAIR (16 < d <= 32, two lanes per chain, samplers.hpp PairChain): the first S = 4 ceil(ceil(d/4)/2)
    coordinates left to right, the rest left to right, then (first) + (second) */
@@ -265,6 +268,14 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
                 double z = resid * isn;
                 term = -0.5 * (z * z + ORC_LOG2PI) - logsn;       /* resid ~ Normal(0, sn) */
                 r = resid * is2n;                                 /* -d/dresid, MCMCDerivRules.jl:57 */
+            } else if (m->kind == ORC_MODEL_PROBIT) {
+                /* examples/probit_regression.jl:26-40: dot(logcdf(N, X pars), y) + dot(logcdf(N, -X pars), 1 - y),
+                   per observation here; d/deta = y exp(A - logcdf(eta)) - (1 - y) exp(A - logcdf(-eta)),
+                   A = -(eta^2 + log(2 pi))/2 (the example's grad_log_posterior) */
+                const double la = orc_normlogcdf(eta), lb = orc_normlogcdf(-eta);
+                term = y * la + (1.0 - y) * lb;
+                const double A = (-(eta * eta + ORC_LOG2PI)) / 2.0;
+                r = y * orc_exp(A - la) - (1.0 - y) * orc_exp(A - lb);
             } else {
                 double tt = orc_exp_tab(-(sgn * eta));            /* prob = 1/(1+exp(-X*vars)) */
                 double p = 1.0 / (1.0 + tt);
@@ -379,7 +390,7 @@ static double orc_eval(const orc_model* m, const double* x, double* g, double* t
             for (int j = 0; j < d; ++j) g[j] = oos ? 0.0 : orc_dist_grad(m->dist, m->mu, m->sigma, x[j]);
         return lp;
     }
-    if (m->kind == ORC_MODEL_LOGISTIC || m->kind == ORC_MODEL_LINEAR) return orc_glm_eval(m, x, g, tmp);
+    if (orc_is_glm(m)) return orc_glm_eval(m, x, g, tmp);
     if (m->kind == ORC_MODEL_ISO) {
         /* model(v -> -dot(v,v), grad = v -> -2v)  README.md:60,63; test/test_syntax.jl:40-41 */
         double lp = -orc_dot(x, m, order);
@@ -836,6 +847,10 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
             case 15: r = a > orc_log(y[i]) ? 1.0 : 0.0; break;    /* RWM.jl:63's test; device: gt_det_log */
             case 16: r = -2.0 * orc_bm_log_u32((uint32_t)(uint64_t)a); break;   /* device: bm_rad2_u32 */
             case 17: r = orc_bm_radius_u32((uint32_t)(uint64_t)a); break;       /* device: bm_radius_u32 */
+            case 18: r = orc_erfc(a); break;
+            case 19: r = orc_log1p(a); break;
+            case 20: r = orc_normlogcdf(a); break;
+            case 21: r = orc_bm_radius_u32((uint32_t)(uint64_t)a); break;       /* device: the LDS-table path */
             case 8: {
                 uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
                 uint32_t key[2] = {0u, 0u}, w[4];

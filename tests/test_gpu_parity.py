@@ -5,6 +5,8 @@ bits bit-identical.  The build's arithmetic is specified operation by operation
 (DESIGN.md §3-4), so in practice samples are compared bit for bit; the 1e-10
 tolerance is the stated fallback and is asserted too.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -54,7 +56,8 @@ def _dev_math(op, x, y=None):
                                      (5, "div"), (7, "round"), (9, "bm_log_u32"), (10, "sin2pi_u32"),
                                      (11, "cos2pi_u32"), (12, "sqrt_pos_normal"), (13, "exp_tab"),
                                      (14, "log_tab"), (16, "bm_rad2_u32"),
-                                     (17, "bm_radius_u32")])
+                                     (17, "bm_radius_u32"), (18, "erfc"), (19, "log1p"),
+                                     (20, "normlogcdf"), (21, "bm_radius_u32_lds")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -70,11 +73,21 @@ def test_device_detmath_bitwise(gpu, op, name):
                             -2.0 * np.log((np.arange(0, 4000) + 0.5) * 2.0**-32),
                             -2.0 * np.log((2.0**32 - 0.5 - np.arange(0, 4000)) * 2.0**-32),
                             np.nextafter(np.arange(1.0, 47.0) ** 2, 0), np.arange(1.0, 47.0) ** 2])
-    elif op in (9, 10, 11, 16, 17):  # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
+    elif op in (18, 20):         # erfc / normal log-cdf: every interval edge, the underflow end, special values
+        edges = np.concatenate([[0.5], (2.0 ** np.arange(-1, 8)[:, None] * (1 + np.arange(4) / 4)).ravel()])
+        x = np.concatenate([rng.uniform(-40, 40, 200000), rng.uniform(-2, 2, 100000), edges, -edges,
+                            np.nextafter(edges, 0), np.nextafter(-edges, 0), rng.uniform(-60, 60, 20000),
+                            [0.0, -0.0, np.inf, -np.inf, np.nan, 1e-300, -1e-300, 27.2, 26.6, -38.5, -37.6]])
+        if op == 20:
+            x = x * np.sqrt(2.0)
+    elif op == 19:
+        x = np.concatenate([-np.exp(rng.uniform(-745, -1e-9, 100000)), rng.uniform(-0.99, 0.0, 100000),
+                            [0.0, -0.0, 1e-300, -1e-17, -0.5, -0.84, np.nan]])
+    elif op in (9, 10, 11, 16, 17, 21):  # 32-bit draws; the device's integer quarter-turn reduction vs the oracle's
         x = np.concatenate([np.floor(rng.uniform(0, 2**32, 200000)), np.arange(0, 2000),
                             2.0**32 - 1 - np.arange(0, 2000), (np.arange(-40, 40) + 2**29 * np.arange(1, 8)[:, None]
                                                                ).ravel() % 2**32])
-        if op == 17:             # every polynomial segment's two ends on both sides, and the tail's edge (v = 2^21)
+        if op in (17, 21):       # every polynomial segment's two ends on both sides, and the tail's edge (v = 2^21)
             e, k = np.meshgrid(np.arange(21, 31), np.arange(32))
             v = (2.0**e * (1 + k / 32)).ravel().astype(np.int64)
             v = np.concatenate([v - 2, v - 1, v, v + 1, [2**21 - 2, 2**21 - 1, 2**21, 2**21 + 1, 2**31 - 1]])
@@ -300,6 +313,9 @@ def _glm_model(kind, d, n=50, seed=0):
     if kind == "logistic":
         Y = (rng.random(n) < 1 / (1 + np.exp(-X @ beta0))).astype(float)
         return mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(d), gradient=True)
+    if kind == "probit":
+        Y = (rng.normal(size=n) < X @ beta0).astype(float)
+        return mc.model(mc.ProbitRegression(X, Y, prior_sigma=10.0), vars=np.zeros(d), gradient=True)
     Y = X @ beta0 + rng.normal(size=n)
     return mc.model(mc.LinearRegression(X, Y, prior_sigma=1.0, noise_sigma=1.0), vars=np.zeros(d), gradient=True)
 
@@ -329,7 +345,28 @@ def test_glm_sampler_parity(gpu, sname, kind, d):
     assert chain.task.evals == int(oc.n_evals.sum())        # leapfrog / evaluation bookkeeping
 
 
-@pytest.mark.parametrize("kind", ["logistic", "linear"])
+@pytest.mark.parametrize("sname", list(GLM_SAMPLERS))
+@pytest.mark.parametrize("d", [3, 37, 200])              # single slice (NM = 1, 4) and d-sliced (4 x 64)
+def test_probit_sampler_parity(gpu, sname, d):
+    """examples/probit_regression.jl's target on every gradient sampler, bitwise against the oracle."""
+    test_glm_sampler_parity(gpu, sname, "probit", d)
+
+
+def test_probit_vaso_example_bitwise(gpu):
+    """The probit example itself (probit_regression.jl:7-16, 68): vaso.txt standardised, MvNormal(0, 100 I) prior,
+    RWM(0.5) x SerialMC(1001:10000), 64 chains from a prior draw (randprior), bitwise against the oracle."""
+    X, Y = mc.vaso_data(os.path.join(os.path.dirname(__file__), "golden", "vaso.txt"))
+    init = np.random.default_rng(68).normal(size=3) * 10.0
+    m = mc.model(mc.ProbitRegression(X, Y), vars=init, gradient=True)
+    r = mc.SerialMC(steps=10000, burnin=1000)
+    chain = mc.run((m * mc.RWM(0.5) * r).batch(64, seed=68))
+    oc = orc.OracleChains(m, mc.RWM(0.5), nchains=64, seed=68)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, "rwm")
+    assert 0.05 < acc_ref.mean() < 0.6
+
+
+@pytest.mark.parametrize("kind", ["logistic", "linear", "probit"])
 @pytest.mark.parametrize("d", [10, 130, 700])
 def test_glm_eval_matches_oracle(gpu, kind, d):
     m = _glm_model(kind, d, n=70)

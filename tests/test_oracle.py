@@ -562,3 +562,101 @@ def test_dist_dsl_logpdf_gradient_and_support(name, params, ref, rng_):
         xo[2] = lo[name]
         lpo, go = orc.eval_batch(m, xo)
         assert lpo[0] == -np.inf and np.all(go == 0.0)
+
+
+def test_erfc_and_normal_logcdf_accuracy():
+    """The probit model's erfc and logcdf(Normal(), z) (oracle/detmath.h orc_erfc / orc_normlogcdf; the device's
+    det_erfc / det_normlogcdf are bitwise the same, test_gpu_parity.py) against 40-digit mpmath: relative error
+    <= 8e-16 for erfc wherever it is normal, <= 2e-15 for the log-cdf of the rounded argument z/sqrt2 where
+    |logcdf| > 1e-300 (z >= -1), of z itself below (StatsFuns's erfcx form, finite down to z^2 overflow)."""
+    import mpmath as mp
+    mp.mp.dps = 40
+    rng = np.random.default_rng(18)
+    x = np.concatenate([rng.uniform(-6, 26, 6000), rng.uniform(-0.6, 0.6, 1000),
+                        2.0 ** np.arange(-1, 5)[:, None].ravel(), [0.0, 1e-300, 0.4999999999999999]])
+    e = orc.detmath(18, x)
+    ref = np.array([float(mp.erfc(mp.mpf(v))) for v in x])
+    ok = ref > 2.3e-308
+    rel = np.abs(e[ok] - ref[ok]) / ref[ok]
+    assert rel.max() <= 8e-16, (rel.max(), x[ok][np.argmax(rel)])
+    z = np.concatenate([rng.uniform(-37, 9, 6000), rng.uniform(-1.5, 1.5, 1000), -np.exp(rng.uniform(0, 300, 2000)),
+                        [-1.0, np.nextafter(-1.0, 0), 0.0, -181.0, -181.1]])
+    lc = orc.detmath(20, z)
+    s2 = float.fromhex("0x1.6a09e667f3bcdp-1")   # RN(1/sqrt2): the argument's rounding is amplified by 2 x^2
+
+    def exact(v):
+        return mp.log(mp.ncdf(mp.mpf(v))) if v < -1 else mp.log1p(-mp.erfc(mp.mpf(v * s2)) / 2)
+    rl = np.array([float(exact(v)) for v in z])
+    ok = np.abs(rl) > 1e-300
+    rel = np.abs(lc[ok] - rl[ok]) / np.abs(rl[ok])
+    assert rel.max() <= 4e-15, (rel.max(), z[ok][np.argmax(rel)])
+    assert orc.detmath(20, np.array([-1e200]))[0] == -np.inf
+    assert orc.detmath(18, np.array([np.nan, -np.inf, np.inf])).tolist()[1:] == [2.0, 0.0]
+
+
+# ------------------------------------------------------------------ probit regression (examples/probit_regression.jl)
+VASO = os.path.join(os.path.dirname(__file__), "golden", "vaso.txt")     # the example's data file, kept as a fixture
+
+
+def _probit_reference(X, Y, B, prior_sd=10.0):
+    """examples/probit_regression.jl:18-40 restated with scipy: logpdf(MvNormal(0, priorvar I), pars) +
+    dot(logcdf(N, X pars), y) + dot(logcdf(N, -X pars), 1 - y), and grad_log_posterior."""
+    d = X.shape[1]
+    lp, g = [], []
+    mvn = stats.multivariate_normal(np.zeros(d), prior_sd**2 * np.eye(d))
+    for b in B.T:
+        xp = X @ b
+        la, lb = stats.norm.logcdf(xp), stats.norm.logcdf(-xp)
+        lp.append(mvn.logpdf(b) + la @ Y + lb @ (1 - Y))
+        A = -(xp**2 + np.log(2 * np.pi)) / 2
+        g.append(X.T @ (Y * np.exp(A - la) - (1 - Y) * np.exp(A - lb)) - b / prior_sd**2)
+    return np.array(lp), np.array(g).T
+
+
+def test_probit_eval_matches_reference_formula_on_vaso():
+    """The probit example's own data (vaso.txt, standardised as the example does) and parameter points drawn from
+    its prior (randprior, MvNormal(0, 100 I)) and around the posterior: the oracle's log-posterior and gradient
+    against the example's formulas evaluated independently (scipy's logcdf and MvNormal)."""
+    X, Y = mc.vaso_data(VASO)
+    m = mc.model(mc.ProbitRegression(X, Y), vars=np.zeros(3), gradient=True)
+    rng = np.random.default_rng(26)
+    B = np.hstack([rng.normal(size=(3, 20)) * 10.0, rng.normal(size=(3, 20)) + np.array([[-2.9], [4.6], [3.6]]),
+                   np.zeros((3, 1))])
+    lp, g = orc.eval_batch(m, B)
+    lr, gr = _probit_reference(X, Y, B)
+    ok = np.isfinite(lr)
+    np.testing.assert_allclose(lp[ok], lr[ok], rtol=1e-12)
+    np.testing.assert_allclose(g[:, ok], gr[:, ok], rtol=1e-9, atol=1e-9)
+
+
+def test_probit_gradient_finite_difference():
+    """helper_diff.jl:8-37's check on the probit target."""
+    X, Y = mc.vaso_data(VASO)
+    m = mc.model(mc.ProbitRegression(X, Y), vars=np.zeros(3), gradient=True)
+    x0 = np.array([[-1.0], [2.0], [1.5]])
+    lp0, g0 = orc.eval_batch(m, x0)
+    for j in range(3):
+        x1 = x0.copy()
+        x1[j] += 1e-7
+        gn = (orc.eval_batch(m, x1)[0] - lp0) / 1e-7
+        assert abs(g0[j, 0] - gn[0]) / max(2e-2, abs(g0[j, 0])) < 2e-3
+
+
+def test_probit_posterior_mean_rwm():
+    """The example's first run, RWM(0.5) x SerialMC(1001:10000) (probit_regression.jl:68), on 64 oracle chains from
+    the posterior mode's neighbourhood: the pooled posterior mean agrees with a direct quadrature-free estimate, the
+    importance-weighted mean of 200 000 prior-free draws from a wide normal (independent of the sampler)."""
+    X, Y = mc.vaso_data(VASO)
+    m = mc.model(mc.ProbitRegression(X, Y), vars=np.array([-2.0, 3.0, 2.5]), gradient=True)
+    oc = orc.OracleChains(m, mc.RWM(0.5), nchains=64, seed=3)
+    s, _, acc = oc.run(mc.SerialMC(steps=10000, burnin=1000, thinning=10))
+    post = s.mean(axis=(0, 2))
+    rng = np.random.default_rng(7)
+    cen, sd = np.array([-2.9, 4.6, 3.6]), np.array([1.5, 2.5, 2.0])
+    Z = cen + sd * rng.normal(size=(200000, 3))
+    lq = stats.norm(cen, sd).logpdf(Z).sum(1)
+    lp, _ = orc.eval_batch(m, Z.T)
+    w = np.exp(lp - lq - (lp - lq).max())
+    ref = (w[:, None] * Z).sum(0) / w.sum()
+    np.testing.assert_allclose(post, ref, atol=0.35)
+    assert 0.05 < acc.mean() < 0.6
