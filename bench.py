@@ -62,6 +62,12 @@ CONFIGS = {
     "binomial": dict(model="logistic", d=10, n=1000, chains=1 << 18, sampler="rwm", steps=100, warmup=10,
                      thinning=1, desc="benchmarks/benchunits/binomial.jl: logistic regression n=1000 d=10, "
                                       "RWM(0.1), 100 steps (the reference's published unit, run batched)"),
+    # the reference's second published benchmark unit (benchmarks/benchunits/bare_distribs.jl:7-27,
+    # benchlog.csv:298-300): y = x * v; y ~ Normal(1, 1) over v = ones(1000), scalar x from the mean, RWM(0.1)
+    "bare_normal": dict(model="distobs", dist=("Normal", 1.0, 1.0), d=1, chains=1 << 20, sampler="rwm", steps=100,
+                        warmup=10, thinning=1, desc="benchmarks/benchunits/bare_distribs.jl: y = x * v; "
+                                                    "y ~ Normal(1, 1), v = ones(1000), RWM(0.1), 100 steps (the "
+                                                    "reference's published unit, run batched)"),
     # the adaptive RAM sampler (not a BASELINE config)
     "ram32": dict(model="iso", d=32, chains=1 << 18, sampler="ram", steps=200, warmup=20, thinning=10,
                   desc="RAM(1., 0.234) on d=32 iso-Normal, 262,144 chains (a 32x32 jump factor per chain)"),
@@ -110,6 +116,9 @@ def regression_data(kind, n, d, key=0x5EED):
 
 
 def build_model(mc, cfg, d):
+    if cfg["model"] == "distobs":                    # bare_distribs.jl:8-16: start at the distribution's mean
+        name, p1, p2 = cfg["dist"]
+        return mc.model(mc.DistObsDSL(name, p1, p2, v=np.ones(1000)), x=p1, gradient=True)
     if cfg["model"] == "iso":
         return mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
     X, Y = regression_data(cfg["model"], cfg["n"], d)
@@ -189,6 +198,32 @@ def measured_valu(kname, wkey):
                 and e.get("workload_key") == wkey):
             return e
     return None
+
+
+# The metric kernel's VALU floor ("VALU floor"): the lane-operations RWM(0.1) on the d = 32
+# iso-Normal needs per chain-step, one instruction each, no moves, address or select overhead --
+# Philox4x32-10: 8.5 blocks (32 normals + half an accept block) x 10 rounds x (2 v_mad_u64_u32 + 2 v_xor3) = 340;
+# Box-Muller radius: 16 x (7 FMAs + conversion, residual, 3 index ops) = 192; angle: 16 x (conversion, index, 4 + 3
+# polynomial FMAs, 2 products with the radius) = 176; proposal x + z*scale, two roundings (RWM.jl:59): 64;
+# log-target -dot(v, v): 32 FMAs + pair combine + negate = 35; accept: 52-bit uniform, screened log, decision and
+# the 16 64-bit moves of an accepted state = 40 -> 847 lane-operations = 13.23 wave instructions per chain-step.
+VALU_FLOOR_METRIC = {"lane_ops_per_chain_step": {"philox": 340, "radius": 192, "angle": 176, "proposal": 64,
+                                                 "log_target": 35, "accept": 40}}
+VALU_FLOOR_METRIC["insts_per_chain_step"] = sum(VALU_FLOOR_METRIC["lane_ops_per_chain_step"].values()) / 64.0
+
+
+def valu_floor(args, vm):
+    """valu_floor / floor_frac of the metric workload (d = 32 iso-Normal RWM): the floor above against the measured
+    VALU instructions per chain-step of the committed PMC profile (quad-cycles per chain-step / quad-cycles per
+    instruction); None for other workloads."""
+    if args.config != "metric" or args.sampler != "rwm" or args.d != 32:
+        return None
+    meas = vm["valu_quadcycles_per_chain_step"] / vm["quadcycles_per_valu_inst"]
+    fl = VALU_FLOOR_METRIC["insts_per_chain_step"]
+    return {"floor_insts_per_chain_step": fl, "measured_insts_per_chain_step": meas, "floor_frac": fl / meas,
+            "lane_ops_per_chain_step": VALU_FLOOR_METRIC["lane_ops_per_chain_step"],
+            "note": "floor = the arithmetic the RWM step needs at one lane-operation each (DESIGN.md §5.1b), / 64 "
+                    "lanes; measured from the committed SQ_INSTS / SQ_ACTIVE_INST_VALU profile of this kernel"}
 
 
 def glm_src_hash():
@@ -295,7 +330,16 @@ def cpu_baseline(model, sampler, seconds, C=4096, leaps_per_step=None):
                       f"so the rate is per chain-step)"}
 
 
-def binomial_units(mc, model, C, local):
+BENCHLOG_REFERENCE = {
+    "binomial": {"source": "benchmarks/benchlog.csv:350-352 (binomial 10x1000, CodeHash 276db306bb, Windows, "
+                           "2 CPU cores, 2013-08-29)", "eval_ms": 0.25765, "evalallg_ms": 0.74805, "rwm100_ms": 25.690},
+    "bare_normal": {"source": "benchmarks/benchlog.csv:298-300 (:(Normal(1,1)) on vector of 1000, CodeHash "
+                              "276db306bb, Windows, 2 CPU cores, 2013-08-29)",
+                    "eval_ms": 0.60083, "evalallg_ms": 0.64702, "rwm100_ms": 61.634},
+}
+
+
+def binomial_units(mc, model, C, local, config="binomial"):
     """The reference's benchmark unit benchmarks/benchunits/binomial.jl:21-27 on this build, for context beside
     benchlog.csv:350-352 (0.258 ms loglik eval, 0.748 ms loglik + gradient, 25.69 ms per 100 RWM steps of one
     chain; 2-core Windows CPU, 2013): the host API's batched model.eval / model.evalallg (mcmc_model_eval: host
@@ -332,10 +376,8 @@ def binomial_units(mc, model, C, local):
         mc.run(t1)
         times.append(time.perf_counter() - t0)
     out["rwm100_1chain_ms"] = {"avg": 1e3 * sum(times) / len(times), "min": 1e3 * min(times)}
-    out["reference"] = {"source": "benchmarks/benchlog.csv:350-352 (binomial 10x1000, CodeHash 276db306bb, "
-                                  "Windows, 2 CPU cores, 2013-08-29)",
-                        "eval_ms": 0.25765, "evalallg_ms": 0.74805, "rwm100_ms": 25.690,
-                        "note": "context, not the target: one 2013 CPU core pair, one chain"}
+    out["reference"] = dict(BENCHLOG_REFERENCE[config], note="context, not the target: one 2013 CPU core pair, "
+                                                             "one chain")
     return out
 
 
@@ -591,7 +633,7 @@ def main():
     traffic = tdet["bytes_per_launch"] if tdet else None
     avg_launch_s = kernel_ms * 1e-3 / launches          # HIP events around the launches, on their stream
     units = C * K / launches                            # chain-steps per launch
-    if cfg0["model"] == "iso":
+    if cfg0["model"] in ("iso", "distobs"):
         # HBM: the fused kernel reads and writes the chain state once per launch (x [d][C], lp [C]) and
         # streams the kept samples (+ gradients) and accept bits; SURVEY.md §8(d)'s per-step state round trip
         # (16 d + 16 + 1/8 B per chain-step) is what an unfused step would move, kept as `survey_bytes`
@@ -625,6 +667,7 @@ def main():
                     "valu_cycles_per_unit": cyc, "valu_busy_measured": vm["valu_busy"],
                     "clock_ghz_measured": vm["clock_ghz"], "valu_source": vm["source"],
                     "hbm": hbm, "survey_bytes": survey_bytes,
+                    "valu_floor": valu_floor(args, vm),
                     "note": "units = chain-steps; VALU cycles per unit from rocprofv3 PMC (SQ_ACTIVE_INST_VALU); "
                             "valu_busy_measured = SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES of that profile (at "
                             "the measured clock); HBM moves only the per-launch state and the kept outputs "
@@ -661,7 +704,7 @@ def main():
     # acceptance over the timed run's kept steps (accept bits, SerialMC.jl:55-63)
     pop8 = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.float64, device=dev)
     acceptance = float(pop8[bits.view(torch.uint8).long()].sum()) / max(1, nkept * C)
-    if cfg0["model"] != "iso":
+    if cfg0["model"] not in ("iso", "distobs"):
         roof["leapfrogs_per_chain_step" if args.sampler in ("hmc", "hmcda") else "evals_per_chain_step"] = \
             evals / (C * K)
         roof["chain_evals_per_s"] = evals * world / T
@@ -679,7 +722,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (chains start at model.init; Philox4x32-10 streams, seed 1"
-                + ("; regression data from numpy Philox, key 0x5EED)" if cfg0["model"] != "iso" else ")"),
+                + ("; regression data from numpy Philox, key 0x5EED)" if cfg0["model"] not in ("iso", "distobs")
+                   else ")"),
         "config": {
             "workload": f"{args.config}: {cfg0['desc']}; SerialMC(steps={K}, burnin={burnin}, "
                         f"thinning={args.thinning}), {C} chains/GPU, {type(sampler).__name__}",
@@ -695,8 +739,8 @@ def main():
     }
     if adapt is not None:
         line["adaptation"] = adapt
-    if args.config == "binomial" and rank == 0:
-        line["reference_units"] = binomial_units(mc, model, C, local)
+    if args.config in ("binomial", "bare_normal") and rank == 0:
+        line["reference_units"] = binomial_units(mc, model, C, local, args.config)
     if pcie is not None:
         line["pcie_inclusive"] = pcie
     if gather is not None:

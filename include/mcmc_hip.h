@@ -68,8 +68,10 @@ enum {
     MCMC_MODEL_LINEAR = 4,           /* examples/linear_regression.jl:14-20  (DSL, gradient=true)    */
     MCMC_MODEL_ABS_NORMAL_DSL = 5,   /* model(:(y = abs(x); y ~ Normal(mu, sigma)))  README.md:246-251 */
     MCMC_MODEL_DIST_DSL = 6,         /* model(:(v ~ Dist(p1, p2))): dist = MCMC_DIST_*, p1 = mu, p2 = sigma */
-    MCMC_MODEL_PROBIT = 7            /* examples/probit_regression.jl:18-40: log-prior MvNormal(0, prior_sigma^2 I)
+    MCMC_MODEL_PROBIT = 7,           /* examples/probit_regression.jl:18-40: log-prior MvNormal(0, prior_sigma^2 I)
                                         + dot(logcdf(N, X pars), Y) + dot(logcdf(N, -X pars), 1 - Y), Y 0.0 / 1.0 */
+    MCMC_MODEL_DIST_OBS = 8          /* model(:(y = x * v; y ~ Dist(p1, p2))), benchmarks/benchunits/bare_distribs.jl:13:
+                                        scalar x (d = 1), data v = Y [n]; dist / mu / sigma as MCMC_MODEL_DIST_DSL */
 };
 
 /* distributions of MCMC_MODEL_DIST_DSL: the DSL's continuous logpdf rules, MCMCDerivRules.jl:56-104

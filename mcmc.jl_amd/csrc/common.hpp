@@ -5,7 +5,8 @@
 namespace mcmc {
 
 enum ModelKind : int32_t {
-    MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4, MK_ABS_NORMAL = 5, MK_DIST = 6, MK_PROBIT = 7
+    MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4, MK_ABS_NORMAL = 5, MK_DIST = 6, MK_PROBIT = 7,
+    MK_DIST_OBS = 8
 };
 // MK_DIST: v ~ Dist(p1, p2) elementwise (MCMCDerivRules.jl:56-104, the DSL's continuous distributions)
 enum DistKind : int32_t {
@@ -56,6 +57,8 @@ struct ChainState {
     int32_t* t_leaps;           // HMC tuned nLeaps
     int32_t* t_acc;             // tuner accepted counter
     int32_t* t_prop;            // tuner proposed counter
+    double* mom;                // regression HMC / HMCDA on d-slices (d > 128): the momentum parked in HBM across each
+                                //   evaluation [d_pad][ld] (glm.hip glm_hmc), so the MFMA loop keeps its registers
     double* ram_L;              // RAM: jump factor S, two halves of packed padded rows [dpad(dpad+1)/2][ram_ld]
     int64_t ram_ld;             // RAM: lane-per-chain: chain stride of ram_L (a multiple of 256); wave-per-chain:
                                 //      doubles per chain (ram.hpp wave layout)

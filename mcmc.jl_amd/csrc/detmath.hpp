@@ -571,13 +571,18 @@ __device__ __forceinline__ void normals4(const u32x4& w, double& z0, double& z1,
 // |L - log u| <= ln2 (2^-23 |log2 u| + 2^-24 log2 e) plus the 1-ulp error of det_log is hundreds of times smaller
 // than E, so a decided test agrees with the exact one.  The rest (probability ~1e-5 per test; u = 0; NaN ratios)
 // takes det_log, on the lanes that need it.
+// The undecided lanes' exact test, out of line: inlined, its det_log polynomial constants were hoisted out of the
+// step loops into VGPRs and spilled (the metric kernel lpp_rwm<4, true, IsoDot, true> stored 64 B a lane to scratch
+// per launch, ~134 MB at 2^21 lanes, to reload them on this 1-in-10^5 path).  A call saves the caller's live
+// registers only on the lanes' rare way in.
+__device__ __attribute__((noinline)) bool gt_det_log_exact(double ratio, double u) { return ratio > det_log(u); }
 __device__ __forceinline__ bool gt_det_log(double ratio, double u) {
     const double L = (double)__builtin_amdgcn_logf((float)u) * 0x1.62e42fefa39efp-1;
     const double E = 0x1p-16 * (1.0 + __builtin_fabs(L));
     const bool sure_acc = ratio > L + E;
     const bool sure_rej = ratio <= L - E;
     bool acc = sure_acc;
-    if (!sure_acc && !sure_rej) acc = ratio > det_log(u);
+    if (!sure_acc && !sure_rej) acc = gt_det_log_exact(ratio, u);
     return acc;
 }
 

@@ -345,6 +345,10 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
         case MCMC_MODEL_ABS_NORMAL_DSL:
             if (!(desc->sigma > 0)) return bail(fail(MCMC_E_INVALID_ARG, "Normal sigma should be > 0"));
             break;
+        case MCMC_MODEL_DIST_OBS:
+            if (d != 1) return bail(fail(MCMC_E_INVALID_ARG, "y = x * v needs a scalar parameter x (d = 1)"));
+            if (desc->n <= 0 || !desc->Y) return bail(fail(MCMC_E_INVALID_ARG, "y = x * v needs the data v (n > 0, Y)"));
+            [[fallthrough]];
         case MCMC_MODEL_DIST_DSL: {
             const double p1 = desc->mu, p2 = desc->sigma;
             const double kPi = 3.14159265358979323846;
@@ -369,6 +373,13 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
             if (!ok) return bail(fail(MCMC_E_INVALID_ARG, "invalid distribution parameters"));
             a.dist = desc->dist;
             a.dconst = c;
+            if (desc->kind == MCMC_MODEL_DIST_OBS) {                    // the data v, read by every chain
+                if (int r = dmalloc(&m->d_Y, (size_t)desc->n)) return bail(r);
+                if (h2d(ctx, m->d_Y, desc->Y, (size_t)desc->n * 8) != hipSuccess)
+                    return bail(fail(MCMC_E_HIP, "model data upload failed"));
+                a.n = desc->n;
+                a.Y = m->d_Y;
+            }
             break;
         }
         case MCMC_MODEL_LOGISTIC:
@@ -443,7 +454,7 @@ extern "C" int mcmc_model_destroy(mcmc_model* m) {
 
 static bool model_is_separable(const mcmc_model* m) {
     return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL || m->args.kind == MK_ABS_NORMAL ||
-           m->args.kind == MK_DIST;
+           m->args.kind == MK_DIST || m->args.kind == MK_DIST_OBS;
 }
 static bool model_is_glm(const mcmc_model* m) {
     return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR || m->args.kind == MK_PROBIT;
@@ -546,7 +557,7 @@ extern "C" int mcmc_model_eval(mcmc_model* m, int64_t nchains, const double* x, 
 static void free_state(mcmc_chains* c) {
     ChainState& s = c->st;
     dfree(s.x); dfree(s.lp); dfree(s.g); dfree(s.t_step); dfree(s.t_bar); dfree(s.t_h);
-    dfree(s.t_leaps); dfree(s.t_acc); dfree(s.t_prop); dfree(s.ram_L);
+    dfree(s.t_leaps); dfree(s.t_acc); dfree(s.t_prop); dfree(s.ram_L); dfree(s.mom);
     s = ChainState{};
 }
 
@@ -705,6 +716,8 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (int r = dmalloc(&c->st.x, nst)) return bail(r);
     if (c->layout == LAYOUT_GLM)                 // gradient at the state (regression targets are not separable)
         if (int r = dmalloc(&c->st.g, nst)) return bail(r);
+    if (c->layout == LAYOUT_GLM && d > 128 && (sa.kind == SK_HMC || sa.kind == SK_HMCDA))   // d-sliced: momentum
+        if (int r = dmalloc(&c->st.mom, (size_t)mcmc_glm_d_pad(d) * c->ld)) return bail(r);      // parking (glm_hmc)
     if (int r = dmalloc(&c->st.lp, nc)) return bail(r);
     const bool tuned = sa.tuner && (sa.kind == SK_MALA || sa.kind == SK_HMC);
     if (tuned || sa.kind == SK_HMCDA)

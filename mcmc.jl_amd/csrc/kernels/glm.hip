@@ -666,9 +666,14 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
 // ------------------------------------------------------------------ state access (layout [d][ld])
 // Lane pointer at coordinate base + 4q; slot (m, e) adds the wave-uniform offset (16m + e) * ld,
 // so the 32 slot addresses cost SGPRs, not VGPRs.
+// The pointer passes through an empty volatile asm at every use: the per-slot addresses derived from it are then
+// formed where they are used instead of being hoisted out of the step / leapfrog loops, where 4 NM 64-bit addresses per
+// state array stayed live across the tile loop and spilled (glm_hmc<8, 4> needed > 1.3 KB of scratch a lane).
 template <class T>
 __device__ __forceinline__ T* glm_lane_ptr(const GlmPos& p, T* base, int64_t ld, int64_t c) {
-    return base + (size_t)(p.base + 4 * p.q) * (size_t)ld + (size_t)c;
+    T* r = base + (size_t)(p.base + 4 * p.q) * (size_t)ld + (size_t)c;
+    asm volatile("" : "+v"(r));
+    return r;
 }
 __device__ __forceinline__ bool glm_valid(const GlmArgs& a, const GlmPos& p, int slot) {
     return own_coord(p, slot) < a.s.d;
@@ -1592,7 +1597,20 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
                 }
             }
             bool oos;
+            // d-slices: the momentum waits in HBM while the evaluation runs (its 4 NM doubles a lane would otherwise
+            // be spilled inside the tile loop at the 256-register budget); plain stores and loads, bitwise the same
+            constexpr bool kPark = NW > 1 && !REC;
+            if (kPark && p.live) {
+                double* mp = glm_lane_ptr(p, a.st.mom, s.ld, p.c);
+#pragma unroll
+                for (int slot = 0; slot < (4 * NM); ++slot) mp[(size_t)(16 * (slot >> 2) + (slot & 3)) * (size_t)s.ld] = m[slot];
+            }
             lpl = glm_eval<NM, NW, true>(a, p, L, x, g, oos);                // calc!(n, ll); same x -> same (lp, g)
+            if (kPark) {
+                const double* mp = glm_lane_ptr(p, a.st.mom, s.ld, p.live ? p.c : 0);
+#pragma unroll
+                for (int slot = 0; slot < (4 * NM); ++slot) m[slot] = mp[(size_t)(16 * (slot >> 2) + (slot & 3)) * (size_t)s.ld];
+            }
             if (active) {
 #pragma unroll
                 for (int slot = 0; slot < (4 * NM); ++slot) m[slot] = m[slot] + (0.5 * g[slot >> 2][slot & 3]) * eps;

@@ -12,6 +12,7 @@ MCMC_LAYOUT_UNIT_DECL(lpc, iso)
 MCMC_LAYOUT_UNIT_DECL(lpc, normal)
 MCMC_LAYOUT_UNIT_DECL(lpc, absnormal)
 MCMC_LAYOUT_UNIT_DECL(lpc, dist)
+MCMC_LAYOUT_UNIT_DECL(lpc, distobs)
 MCMC_LAYOUT_UNIT_DECL(wpc, iso)
 MCMC_LAYOUT_UNIT_DECL(wpc, normal)
 MCMC_LAYOUT_UNIT_DECL(wpc, absnormal)

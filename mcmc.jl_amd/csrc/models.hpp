@@ -141,6 +141,29 @@ struct DistDSL {
     }
 };
 
+// The DSL block `y = x * v; y ~ Dist(p1, p2)` of the reference's bare_distribs benchmark unit
+// (benchmarks/benchunits/bare_distribs.jl:13): a scalar parameter x (d = 1) scaling a data vector v of n entries,
+// log-target sum_i logpdf(D, x v_i) (LLAcc: left to right), d/dx = sum_i v_i dlogpdf(D, x v_i) (the reverse rule of
+// y = x * v).  The data is read by every lane at the same address (a broadcast from L1 / L2).
+struct DistObsDSL {
+    static constexpr const char* kName = "DistObsDSL";
+    static constexpr bool kLLAcc = true;
+    static constexpr bool kHalfGradNeg = false;
+    DistDSL D;
+    const double* v;
+    int64_t n;
+    __device__ explicit DistObsDSL(const ModelArgs& m) : D(m), v(m.Y), n(m.n) {}
+    __device__ __forceinline__ void acc(double& a, double x) const {
+        for (int64_t i = 0; i < n; ++i) a = a + D.logpdf(x * v[i]);
+    }
+    __device__ __forceinline__ double finish(double a) const { return a; }
+    __device__ __forceinline__ double grad(double x) const {
+        double g = 0.0;
+        for (int64_t i = 0; i < n; ++i) g = g + v[i] * D.grad(x * v[i]);
+        return g;
+    }
+};
+
 // LLAcc rule: a non-finite total means out of support -> (-Inf, 0).
 template <class M>
 __device__ __forceinline__ double llacc_finish(const M& m, double a, bool& oos) {

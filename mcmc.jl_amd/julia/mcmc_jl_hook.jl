@@ -49,7 +49,8 @@ type HipOutputs                   # mcmc_outputs (the library writes runtime_s, 
   runtime_s::Float64; kernel_ms::Float64; nkept::Int64
 end
 
-const HIP_MODEL_KINDS = {:isonormal_dot => 1, :normal => 2, :logistic => 3, :linear => 4, :absnormal => 5, :dist => 6}
+const HIP_MODEL_KINDS = {:isonormal_dot => 1, :normal => 2, :logistic => 3, :linear => 4, :absnormal => 5, :dist => 6,
+                         :probit => 7, :dist_obs => 8}
 const HIP_DISTS = {:Normal => 1, :Uniform => 2, :Weibull => 3, :Beta => 4, :TDist => 5, :Exponential => 6,
                    :Gamma => 7, :Cauchy => 8, :LogNormal => 9, :Laplace => 10}
 
@@ -77,15 +78,19 @@ end
 # hipmodel(:logistic; X=X, Y=Y, init=zeros(size(X,2)))          examples/logistic_regression.jl:16-22
 # hipmodel(:linear; X=X, Y=Y)                                   examples/linear_regression.jl:14-20
 # hipmodel(:dist; dist=:Gamma, mu=2., sigma=1., init=ones(3))   model(:(v ~ Gamma(2., 1.)), v=ones(3))
+# hipmodel(:probit; X=X, Y=y, prior_sigma=10.)                  examples/probit_regression.jl:18-40
+# hipmodel(:dist_obs; dist=:Normal, mu=1., sigma=1., Y=ones(1000), init=[1.])
+#                                                               model(:(y = x * v; y ~ Normal(1, 1)), x=1.)
 function hipmodel(kind::Symbol; init::Vector{Float64}=Float64[], scale::Vector{Float64}=Float64[],
                   name::Symbol=:vars, gradient::Bool=true, mu::Float64=0., sigma::Float64=1., dist::Symbol=:Normal,
                   prior_sigma::Float64=1., noise_sigma::Float64=1., link_sign::Float64=1.,
                   X::Matrix{Float64}=zeros(0, 0), Y::Vector{Float64}=Float64[], device::Int=0)
   @assert haskey(HIP_MODEL_KINDS, kind) "unknown GPU model kind $kind"
-  if kind == :logistic || kind == :linear
+  if kind == :logistic || kind == :linear || kind == :probit
     @assert size(X, 1) == length(Y) "X has $(size(X, 1)) rows, Y $(length(Y)) entries"
     isempty(init) && (init = zeros(size(X, 2)))
   end
+  kind == :dist_obs && (@assert length(init) == 1 "y = x * v: x is a scalar"; @assert !isempty(Y) "the data v in Y")
   d = length(init)
   @assert d > 0 "init must hold the parameter vector"
   isempty(scale) && (scale = ones(d))
@@ -100,7 +105,7 @@ function hip_desc(m::MCMCHipModel, Xr::Vector{Float64})
                m.mu, m.sigma, m.prior_sigma, m.noise_sigma, m.link_sign, length(m.Y),
                isempty(Xr) ? convert(Ptr{Float64}, C_NULL) : pointer(Xr),
                isempty(m.Y) ? convert(Ptr{Float64}, C_NULL) : pointer(m.Y),
-               m.kind == :dist ? HIP_DISTS[m.dist] : 0)
+               (m.kind == :dist || m.kind == :dist_obs) ? HIP_DISTS[m.dist] : 0)
 end
 
 # ---- samplers (RWM.jl:24-36, MALA.jl:50-62, HMC.jl:53-74, HMCDA.jl:24-43, RAM.jl:22-35)

@@ -5,7 +5,7 @@ runs in the HIP kernels of libmcmc_hip.so through the C ABI (include/mcmc_hip.h)
 """
 from ._lib import MCMCError, OutOfSupportError, load as load_library, LIB_PATH  # noqa: F401
 from .api import (  # noqa: F401
-    IsoNormalDot, NormalDSL, AbsNormalDSL, DistDSL, LogisticRegression, LinearRegression, ProbitRegression, vaso_data,
+    IsoNormalDot, NormalDSL, AbsNormalDSL, DistDSL, DistObsDSL, LogisticRegression, LinearRegression, ProbitRegression, vaso_data,
     MCMCLikelihoodModel, model,
     RWM, MALA, HMC, HMCDA, RAM, EmpMCTuner, EmpiricalMCMCTuner, SerialMC, MCMCTask, MCMCChain,
     run, resume, device_count,

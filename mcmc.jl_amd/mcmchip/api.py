@@ -30,7 +30,7 @@ from . import _lib
 from ._lib import check, dptr
 
 __all__ = [
-    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "LogisticRegression", "LinearRegression", "ProbitRegression", "vaso_data", "MCMCLikelihoodModel", "model",
+    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "DistObsDSL", "LogisticRegression", "LinearRegression", "ProbitRegression", "vaso_data", "MCMCLikelihoodModel", "model",
     "RWM", "MALA", "HMC", "HMCDA", "RAM", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
     "run", "resume", "device_count",
 ]
@@ -103,6 +103,19 @@ class DistDSL:
             p[i] = float(v)
         self.name, self.dist = dist, _lib.DISTS[dist]
         self.mu, self.sigma = p                         # p1, p2 in the C ABI's mu / sigma slots
+
+
+class DistObsDSL(DistDSL):
+    """The DSL block `y = x * v; y ~ Dist(p1, p2)` of the reference's bare_distribs benchmark unit
+    (benchmarks/benchunits/bare_distribs.jl:13, v = ones(1000) there): a scalar parameter x scaling the data vector v,
+    log-target sum_i logpdf(Dist, x v_i).  v rides in the C ABI's data slots (X = v as one column, Y = v)."""
+    kind = _lib.MODEL_DIST_OBS
+
+    def __init__(self, dist: str, *params: float, v=None):
+        super().__init__(dist, *params)
+        v = np.ones(1000) if v is None else v
+        self.Y = np.ascontiguousarray(np.asarray(v, dtype=np.float64).reshape(-1))
+        self.X = self.Y.reshape(-1, 1)
 
 
 class LogisticRegression:

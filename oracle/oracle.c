@@ -34,6 +34,7 @@
 #define ORC_MODEL_ABS_NORMAL 5
 #define ORC_MODEL_DIST 6
 #define ORC_MODEL_PROBIT 7
+#define ORC_MODEL_DIST_OBS 8
 
 #define ORC_RWM 1
 #define ORC_MALA 2
@@ -380,6 +381,20 @@ static double orc_dist_grad(int dist, double p1, double p2, double v) {
 
 static double orc_eval(const orc_model* m, const double* x, double* g, double* tmp, int order) {
     const int d = m->d;
+    if (m->kind == ORC_MODEL_DIST_OBS) {
+        /* benchmarks/benchunits/bare_distribs.jl:13: y = x * v; y ~ Dist(p1, p2), scalar x, data v = Y [n]: the LLAcc
+           sum left to right, d/dx = sum_i v_i dlogpdf(x v_i) (left to right) */
+        const double c = orc_dist_const(m->dist, m->mu, m->sigma);
+        double lp = 0.0, gx = 0.0;
+        for (int64_t i = 0; i < m->n; ++i) lp = lp + orc_dist_logpdf(m->dist, m->mu, m->sigma, c, x[0] * m->Y[i]);
+        int oos = !isfinite(lp);
+        if (oos) lp = -INFINITY;
+        if (g) {
+            for (int64_t i = 0; i < m->n; ++i) gx = gx + m->Y[i] * orc_dist_grad(m->dist, m->mu, m->sigma, x[0] * m->Y[i]);
+            g[0] = oos ? 0.0 : gx;
+        }
+        return lp;
+    }
     if (m->kind == ORC_MODEL_DIST) {
         const double c = orc_dist_const(m->dist, m->mu, m->sigma);
         for (int j = 0; j < d; ++j) tmp[j] = orc_dist_logpdf(m->dist, m->mu, m->sigma, c, x[j]);

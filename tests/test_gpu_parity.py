@@ -726,3 +726,36 @@ def test_iso_hmc_overflowing_trajectories(gpu, d, eps, nl):
     s, g, acc = oc.run(r)
     assert_parity(ch, s, g, acc, "hmc")
     assert ch.task.evals == int(oc.n_evals.sum())
+
+
+# ------------------------------------------------------------------ y = x * v; y ~ D (bare_distribs.jl)
+from test_oracle import BARE_DISTRIBS, bare_start  # noqa: E402
+
+
+@pytest.mark.parametrize("name,p", BARE_DISTRIBS)
+def test_dist_obs_rwm100_bitwise(gpu, name, p):
+    """benchmarks/benchunits/bare_distribs.jl's "100 RWM steps" unit (run(m * RWM(0.1), steps=100) from the
+    distribution's mean) on 300 chains, and its "loglik and gradient eval", bitwise against the oracle."""
+    m = mc.model(mc.DistObsDSL(name, *p), x=bare_start(name, p), gradient=True)
+    r = mc.SerialMC(steps=100)
+    chain = mc.run((m * mc.RWM(0.1) * r).batch(300, seed=13))
+    oc = orc.OracleChains(m, mc.RWM(0.1), nchains=300, seed=13)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, "rwm")
+    xs = bare_start(name, p) * np.linspace(0.8, 1.2, 33)[None, :]
+    lp, g = m.evalallg(xs)
+    lp_r, g_r = orc.eval_batch(m, xs)
+    assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
+
+
+@pytest.mark.parametrize("sname", ["mala", "hmc", "hmcda"])
+@pytest.mark.parametrize("name,p", [("Normal", (1, 1)), ("Gamma", (3, 0.2)), ("LogNormal", (2, 0.1))])
+def test_dist_obs_gradient_samplers_bitwise(gpu, sname, name, p):
+    v = np.linspace(0.5, 1.5, 200)
+    m = mc.model(mc.DistObsDSL(name, *p, v=v), x=bare_start(name, p), gradient=True)
+    sp = {"mala": lambda: mc.MALA(0.001), "hmc": lambda: mc.HMC(3, 0.005), "hmcda": lambda: mc.HMCDA(len=0.05)}[sname]
+    r = mc.SerialMC(steps=30, burnin=5, thinning=2)
+    chain = mc.run((m * sp() * r).batch(130, seed=4))
+    oc = orc.OracleChains(m, sp(), nchains=130, seed=4)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, sname)

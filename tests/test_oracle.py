@@ -660,3 +660,46 @@ def test_probit_posterior_mean_rwm():
     ref = (w[:, None] * Z).sum(0) / w.sum()
     np.testing.assert_allclose(post, ref, atol=0.35)
     assert 0.05 < acc.mean() < 0.6
+
+
+# ------------------------------------------------------------------ y = x * v; y ~ D (bare_distribs.jl)
+# benchmarks/benchunits/bare_distribs.jl:29-45: the 17 distributions, each started at its mean (Cauchy: 1.0)
+BARE_DISTRIBS = [("Normal", (1, 1)), ("Normal", (3, 12)), ("Weibull", (1, 1)), ("Weibull", (3, 1)),
+                 ("Uniform", (0, 2)), ("TDist", (2.2,)), ("TDist", (4,)), ("Beta", (1, 2)), ("Beta", (3, 2)),
+                 ("Gamma", (1, 2)), ("Gamma", (3, 0.2)), ("Cauchy", (0, 1)), ("Cauchy", (-1, 0.2)),
+                 ("Exponential", (3,)), ("Exponential", (0.2,)), ("LogNormal", (-1, 1)), ("LogNormal", (2, 0.1))]
+
+
+def _scipy_dist(name, p):
+    return {"Normal": lambda: stats.norm(p[0], p[1]), "Weibull": lambda: stats.weibull_min(p[0], scale=p[1]),
+            "Uniform": lambda: stats.uniform(p[0], p[1] - p[0]), "TDist": lambda: stats.t(p[0]),
+            "Beta": lambda: stats.beta(p[0], p[1]), "Gamma": lambda: stats.gamma(p[0], scale=p[1]),
+            "Cauchy": lambda: stats.cauchy(p[0], p[1]), "Exponential": lambda: stats.expon(scale=p[0]),
+            "LogNormal": lambda: stats.lognorm(p[1], scale=np.exp(p[0]))}[name]()
+
+
+def bare_start(name, p):
+    m = _scipy_dist(name, p).mean()
+    return float(m) if np.isfinite(m) else 1.0                 # bare_distribs.jl:10-12
+
+
+@pytest.mark.parametrize("name,p", BARE_DISTRIBS)
+def test_dist_obs_eval_matches_scipy(name, p):
+    """The benchmark unit's model at its start value and around it: lp = sum_i logpdf(D, x v_i) over a 1000-vector v
+    (ones, as the unit, and a non-trivial v), gradient sum_i v_i dlogpdf; against scipy, and by finite differences."""
+    D = _scipy_dist(name, p)
+    x0 = bare_start(name, p)
+    for v in (np.ones(1000), np.linspace(0.5, 1.5, 1000)):
+        m = mc.model(mc.DistObsDSL(name, *p, v=v), x=x0, gradient=True)
+        xs = np.array([[x0, x0 * 0.9, x0 * 1.1 + 0.01]])
+        lp, g = orc.eval_batch(m, xs)
+        ref = np.array([D.logpdf(x * v).sum() for x in xs[0]])
+        ok = np.isfinite(ref)
+        np.testing.assert_allclose(lp[ok], ref[ok], rtol=1e-11)
+        assert (lp[~ok] == -np.inf).all() and (g[0, ~ok] == 0).all()
+        for j in np.nonzero(ok)[0]:
+            h = 1e-7 * max(1.0, abs(xs[0, j]))
+            lp1, _ = orc.eval_batch(m, xs[:, j:j + 1] + h)
+            if np.isfinite(lp1[0]):
+                fd = (lp1[0] - lp[j]) / h
+                assert abs(g[0, j] - fd) <= 2e-3 * max(1.0, abs(fd)), (name, p, xs[0, j], g[0, j], fd)
