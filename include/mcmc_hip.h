@@ -70,8 +70,11 @@ enum {
     MCMC_MODEL_DIST_DSL = 6,         /* model(:(v ~ Dist(p1, p2))): dist = MCMC_DIST_*, p1 = mu, p2 = sigma */
     MCMC_MODEL_PROBIT = 7,           /* examples/probit_regression.jl:18-40: log-prior MvNormal(0, prior_sigma^2 I)
                                         + dot(logcdf(N, X pars), Y) + dot(logcdf(N, -X pars), 1 - Y), Y 0.0 / 1.0 */
-    MCMC_MODEL_DIST_OBS = 8          /* model(:(y = x * v; y ~ Dist(p1, p2))), benchmarks/benchunits/bare_distribs.jl:13:
+    MCMC_MODEL_DIST_OBS = 8,         /* model(:(y = x * v; y ~ Dist(p1, p2))), benchmarks/benchunits/bare_distribs.jl:13:
                                         scalar x (d = 1), data v = Y [n]; dist / mu / sigma as MCMC_MODEL_DIST_DSL */
+    MCMC_MODEL_OU = 9                /* examples/ornstein.jl:19-30: pars (tau, sigma, mu) (d = 3), the series x = Y [n],
+                                        n >= 2: tau ~ Uniform(0,100), sigma ~ Uniform(0,2), mu ~ Uniform(0,20),
+                                        resid = x[2:end] - x[1:end-1] exp(-1/tau) - mu (1 - exp(-1/tau)) ~ Normal(0, sigma) */
 };
 
 /* distributions of MCMC_MODEL_DIST_DSL: the DSL's continuous logpdf rules, MCMCDerivRules.jl:56-104

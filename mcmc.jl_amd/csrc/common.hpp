@@ -6,7 +6,7 @@ namespace mcmc {
 
 enum ModelKind : int32_t {
     MK_ISO = 1, MK_NORMAL = 2, MK_LOGISTIC = 3, MK_LINEAR = 4, MK_ABS_NORMAL = 5, MK_DIST = 6, MK_PROBIT = 7,
-    MK_DIST_OBS = 8
+    MK_DIST_OBS = 8, MK_OU = 9
 };
 // MK_DIST: v ~ Dist(p1, p2) elementwise (MCMCDerivRules.jl:56-104, the DSL's continuous distributions)
 enum DistKind : int32_t {

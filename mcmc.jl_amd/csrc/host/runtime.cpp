@@ -382,6 +382,19 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
             }
             break;
         }
+        case MCMC_MODEL_OU: {
+            // examples/ornstein.jl:19-30; the prior part of the LLAcc sum, ((0 + logpdf(Uniform(0, 100), tau)) +
+            // logpdf(Uniform(0, 2), sigma)) + logpdf(Uniform(0, 20), mu) inside the support, -log(b - a) each
+            if (d != 3) return bail(fail(MCMC_E_INVALID_ARG, "the Ornstein-Uhlenbeck model has 3 parameters (tau, sigma, mu)"));
+            if (desc->n < 2 || !desc->Y) return bail(fail(MCMC_E_INVALID_ARG, "the Ornstein-Uhlenbeck model needs a series of n >= 2 values (Y)"));
+            a.dconst = ((0.0 + -std::log(100.0)) + -std::log(2.0)) + -std::log(20.0);
+            if (int r = dmalloc(&m->d_Y, (size_t)desc->n)) return bail(r);
+            if (h2d(ctx, m->d_Y, desc->Y, (size_t)desc->n * 8) != hipSuccess)
+                return bail(fail(MCMC_E_HIP, "model data upload failed"));
+            a.n = desc->n;
+            a.Y = m->d_Y;
+            break;
+        }
         case MCMC_MODEL_LOGISTIC:
         case MCMC_MODEL_PROBIT:
         case MCMC_MODEL_LINEAR: {
@@ -452,9 +465,10 @@ extern "C" int mcmc_model_destroy(mcmc_model* m) {
     return MCMC_OK;
 }
 
+// the lane / wave-per-chain kernel families (the joint OU target runs there too, at its fixed d = 3)
 static bool model_is_separable(const mcmc_model* m) {
     return m->args.kind == MK_ISO || m->args.kind == MK_NORMAL || m->args.kind == MK_ABS_NORMAL ||
-           m->args.kind == MK_DIST || m->args.kind == MK_DIST_OBS;
+           m->args.kind == MK_DIST || m->args.kind == MK_DIST_OBS || m->args.kind == MK_OU;
 }
 static bool model_is_glm(const mcmc_model* m) {
     return m->args.kind == MK_LOGISTIC || m->args.kind == MK_LINEAR || m->args.kind == MK_PROBIT;
@@ -740,10 +754,11 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (sa.kind == SK_RAM) {
         // padded width: the lane-per-chain kernel's NC = 4 ceil(d/4), the regression kernel's DF = d_pad
         if (c->layout == LAYOUT_WPC) {
-            // wave-per-chain: [half][chain][column-major packed factor] (ram.hpp wave layout), 4-chain blocks
+            // wave-per-chain: [half][chain][column-major packed factor] (ram.hpp wave layout), one block per chain of
+            // every launched wave (8 chains per workgroup when two chains share a wave)
             c->ram_dpad = d;
             c->st.ram_ld = round_up((int64_t)ram_nrows(d), 8);
-            c->st.ram_hs = round_up(nchains, 4) * c->st.ram_ld;
+            c->st.ram_hs = round_up(nchains, 8) * c->st.ram_ld;
         } else {
             c->ram_dpad = c->layout == LAYOUT_GLM ? mcmc_glm_d_pad(d) : (int)round_up(d, 4);
             c->st.ram_ld = round_up(nchains, 256);

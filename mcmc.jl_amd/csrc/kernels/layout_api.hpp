@@ -13,6 +13,7 @@ MCMC_LAYOUT_UNIT_DECL(lpc, normal)
 MCMC_LAYOUT_UNIT_DECL(lpc, absnormal)
 MCMC_LAYOUT_UNIT_DECL(lpc, dist)
 MCMC_LAYOUT_UNIT_DECL(lpc, distobs)
+MCMC_LAYOUT_UNIT_DECL(lpc, ou)
 MCMC_LAYOUT_UNIT_DECL(wpc, iso)
 MCMC_LAYOUT_UNIT_DECL(wpc, normal)
 MCMC_LAYOUT_UNIT_DECL(wpc, absnormal)
@@ -22,6 +23,7 @@ hipError_t mcmc_lpc_ram_iso(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_lpc_ram_normal(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_lpc_ram_absnormal(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_lpc_ram_dist(const mcmc::KernelArgs& a, hipStream_t st);
+hipError_t mcmc_lpc_ram_ou(const mcmc::KernelArgs& a, hipStream_t st);      // lpc_ram_ou.hip
 // wave-per-chain RAM kernels, 32 < d <= 1024 (wpc_ram.hip)
 hipError_t mcmc_wpc_ram_iso(const mcmc::KernelArgs& a, hipStream_t st);
 hipError_t mcmc_wpc_ram_normal(const mcmc::KernelArgs& a, hipStream_t st);

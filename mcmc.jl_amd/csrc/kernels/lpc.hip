@@ -11,6 +11,7 @@ hipError_t mcmc_launch_lpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
             case MK_NORMAL: return mcmc_lpc_ram_normal(a, st);
             case MK_ABS_NORMAL: return mcmc_lpc_ram_absnormal(a, st);
             case MK_DIST: return mcmc_lpc_ram_dist(a, st);
+            case MK_OU: return mcmc_lpc_ram_ou(a, st);
             default: return hipErrorInvalidValue;
         }
     }
@@ -20,6 +21,7 @@ hipError_t mcmc_launch_lpc_step(const mcmc::KernelArgs& a, hipStream_t st) {
         case MK_ABS_NORMAL: return mcmc_lpc_step_absnormal(a, st);
         case MK_DIST: return mcmc_lpc_step_dist(a, st);
         case MK_DIST_OBS: return mcmc_lpc_step_distobs(a, st);
+        case MK_OU: return mcmc_lpc_step_ou(a, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -34,6 +36,7 @@ hipError_t mcmc_launch_lpc_eval(const mcmc::KernelArgs& a, const double* xin, do
         case MK_ABS_NORMAL: return mcmc_lpc_eval_absnormal(a, xin, lp, g, check, st);
         case MK_DIST: return mcmc_lpc_eval_dist(a, xin, lp, g, check, st);
         case MK_DIST_OBS: return mcmc_lpc_eval_distobs(a, xin, lp, g, check, st);
+        case MK_OU: return mcmc_lpc_eval_ou(a, xin, lp, g, check, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -47,6 +50,7 @@ hipError_t mcmc_launch_lpc_record(const mcmc::KernelArgs& a, const mcmc::LeapRec
         case MK_ABS_NORMAL: return mcmc_lpc_record_absnormal(a, r, st);
         case MK_DIST: return mcmc_lpc_record_dist(a, r, st);
         case MK_DIST_OBS: return mcmc_lpc_record_distobs(a, r, st);
+        case MK_OU: return mcmc_lpc_record_ou(a, r, st);
         default: return hipErrorInvalidValue;
     }
 }

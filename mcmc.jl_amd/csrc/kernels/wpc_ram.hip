@@ -1,5 +1,6 @@
 // wpc_ram.hip -- wave-per-chain RAM kernels (src/samplers/RAM.jl:41-79) for 32 < d <= 1024, every separable
-// model kind: samplers.hpp ram_wave_body over the ram.hpp wave layout of the jump factor.
+// model kind: samplers.hpp ram_wave_body over the ram.hpp wave layout of the jump factor (two chains per wave up to
+// d = 256, one beyond).
 #include "wpc_impl.hpp"
 
 namespace mcmc {
@@ -7,13 +8,28 @@ namespace mcmc {
 template <int G, class M>
 __global__ __launch_bounds__(kBlock) void wpc_ram(KernelArgs a) { ram_wave_body<WaveChain<G, false>, M>(a); }
 
+// 32 < d <= 256: two chains per wave (HalfWaveChain), so a column's pivot (three readlanes, a square root and three
+// divisions) serves two chains' rows; G slot groups of 128 coordinates
+template <int G, class M>
+__global__ __launch_bounds__(kBlock) void wpc_ram2(KernelArgs a) { ram_wave_body<HalfWaveChain<G>, M>(a); }
+
+constexpr int kRamHalfMaxD = 256;
+
 template <class M>
 static hipError_t wpc_ram_step(const KernelArgs& a, hipStream_t st) {
+    if (a.s.d <= kRamHalfMaxD) {
+        constexpr int cpb = 2 * kChainsPerBlock;
+        const dim3 grid((unsigned)((a.s.C + cpb - 1) / cpb));
+        const int g = a.s.d <= 128 ? 1 : 2;
+        mcmc_note_step_kernel("wpc_ram2<%d, %s>", g, M::kName);
+        if (g == 1) wpc_ram2<1, M><<<grid, kBlock, 0, st>>>(a);
+        else wpc_ram2<2, M><<<grid, kBlock, 0, st>>>(a);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)((a.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
     const int g = wpc_nb_for(a.s.d);
     mcmc_note_step_kernel("wpc_ram<%d, %s>", g, M::kName);
     switch (g) {
-        case 1: wpc_ram<1, M><<<grid, kBlock, 0, st>>>(a); break;
         case 2: wpc_ram<2, M><<<grid, kBlock, 0, st>>>(a); break;
         case 4: wpc_ram<4, M><<<grid, kBlock, 0, st>>>(a); break;
         default: return hipErrorInvalidValue;

@@ -25,6 +25,7 @@
 // (DESIGN.md §4).  Accumulation is `acc = fma(v, v, acc)` for the dot product
 // and `acc = acc + term` for logpdf sums.
 #pragma once
+#include <type_traits>
 #include "common.hpp"
 #include "detmath.hpp"
 
@@ -163,6 +164,84 @@ struct DistObsDSL {
         return g;
     }
 };
+
+// The Ornstein-Uhlenbeck model of examples/ornstein.jl:19-30 -- a joint (non-separable) target over
+// v = (tau, sigma, mu) and a series y[0..n-1]:
+//     tau ~ Uniform(0, 100); sigma ~ Uniform(0, 2); mu ~ Uniform(0, 20)
+//     fac = exp(-1/tau); resid = y[2:end] - y[1:end-1] * fac - mu * (1 - fac); resid ~ Normal(0, sigma)
+// LLAcc order: ((0 + logpdf(U, tau)) + logpdf(U, sigma)) + logpdf(U, mu) is the host constant c0 (-log(b - a) each,
+// glibc log), then + sum(logpdf(Normal(0, sigma), resid)) summed left to right; an out-of-support prior is -Inf
+// (AccumulatorDerivRules.jl:12-20).  Gradient: reverse mode through the expression with the DSL's rules
+// (MCMCDerivRules.jl:57-59 Normal dx / dsigma, :62 Uniform dx = 0):
+//     dr_i = (0 - r_i) / (sigma sigma);  G0 = sum dr_i;  G1 = sum dr_i y_i;  Gs = sum ((r_i r_i) / (sigma sigma) - 1) / sigma
+//     d tau = (mu G0 - G1) (fac / (tau tau));  d sigma = Gs;  d mu = -(G0 (1 - fac))
+// Joint models run lane per chain only (the runtime refuses other widths); the series is read by every lane at the
+// same address (a broadcast).  oracle.c ORC_MODEL_OU is the twin.
+struct OUDSL {
+    static constexpr const char* kName = "OUDSL";
+    static constexpr bool kLLAcc = true;
+    static constexpr bool kHalfGradNeg = false;
+    static constexpr bool kJoint = true;
+    const double* y;
+    int64_t n;
+    double c0;
+    __device__ explicit OUDSL(const ModelArgs& m) : y(m.Y), n(m.n), c0(m.dconst) {}
+    __device__ __forceinline__ static bool in_support(double tau, double sigma, double mu) {
+        return tau >= 0.0 && tau <= 100.0 && sigma >= 0.0 && sigma <= 2.0 && mu >= 0.0 && mu <= 20.0;
+    }
+    template <int NC>
+    __device__ __forceinline__ double joint_lp(const double (&v)[NC], bool& oos) const {
+        const double tau = v[0], sigma = v[1], mu = v[2];
+        oos = true;
+        if (!in_support(tau, sigma, mu)) return -__builtin_inf();
+        const double fac = det_exp(-1.0 / tau);
+        const double c = mu * (1.0 - fac);
+        const double logsig = det_log(sigma);
+        double s = 0.0;
+        double y0 = y[0];
+        for (int64_t i = 1; i < n; ++i) {
+            const double y1 = y[i];
+            const double z = ((y1 - y0 * fac) - c) / sigma;
+            s = s + (-0.5 * (z * z + kLog2Pi) - logsig);
+            y0 = y1;
+        }
+        const double lp = c0 + s;
+        oos = !(lp - lp == 0.0);
+        return oos ? -__builtin_inf() : lp;
+    }
+    template <int NC>
+    __device__ __forceinline__ void joint_grad(const double (&v)[NC], double (&g)[NC]) const {
+        const double tau = v[0], sigma = v[1], mu = v[2];
+        const double fac = det_exp(-1.0 / tau);
+        const double c = mu * (1.0 - fac);
+        const double s2 = sigma * sigma;
+        double g0 = 0.0, g1 = 0.0, gs = 0.0;
+        double y0 = y[0];
+        for (int64_t i = 1; i < n; ++i) {
+            const double y1 = y[i];
+            const double r = (y1 - y0 * fac) - c;
+            const double dr = (0.0 - r) / s2;
+            g0 = g0 + dr;
+            g1 = g1 + dr * y0;
+            gs = gs + ((r * r) / s2 - 1.0) / sigma;
+            y0 = y1;
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k) g[k] = 0.0;
+        g[0] = (mu * g0 - g1) * (fac / (tau * tau));
+        g[1] = gs;
+        g[2] = -(g0 * (1.0 - fac));
+    }
+    // the per-coordinate interface of separable models is never used for a joint model
+    __device__ __forceinline__ void acc(double&, double) const {}
+    __device__ __forceinline__ double finish(double a) const { return a; }
+    __device__ __forceinline__ double grad(double) const { return 0.0; }
+};
+
+template <class M, class = void>
+struct is_joint : std::false_type {};
+template <class M>
+struct is_joint<M, std::void_t<decltype(M::kJoint)>> : std::bool_constant<M::kJoint> {};
 
 // LLAcc rule: a non-finite total means out of support -> (-Inf, 0).
 template <class M>

@@ -147,8 +147,21 @@ __device__ __forceinline__ double ram_readlane(double v, int l) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ ram_rsrc_t ram_chain_rsrc(const double* block, int64_t ld) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(block), (short)0, (int)(ld * 8), 0x00020000);
+// the factor blocks of a wave's chains (one block, or the two adjacent blocks of a HalfWaveChain pair)
+__device__ __forceinline__ ram_rsrc_t ram_chain_rsrc(const double* block, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(block), (short)0, (int)bytes, 0x00020000);
+}
+
+// column k's pivot entries from their owner lane j of each chain: one chain per wave (L = 64) reads lane j; two
+// chains per wave (L = 32) read lanes j and 32 + j and each half takes its own
+template <int L>
+__device__ __forceinline__ double ram_bcast(double v, int j) {
+    if constexpr (L == 64) {
+        return ram_readlane(v, j);
+    } else {
+        const double a = ram_readlane(v, j), b = ram_readlane(v, j + 32);
+        return (threadIdx.x & 32) ? b : a;
+    }
 }
 __device__ __forceinline__ double ram_wload(ram_rsrc_t r, uint32_t vo, int so) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
@@ -157,14 +170,14 @@ __device__ __forceinline__ void ram_wstore(ram_rsrc_t r, uint32_t vo, int so, do
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ram_u32x2, v), r, vo, so, 0);
 }
 
-// The columns k = 0..d-1 in order: k = 4 (j + 64 g) + e, owner lane j (runtime, wave-uniform), owner slot 4 g + e
-// (unrolled).  col(k, j, ks) is called once per column.
-template <int G, class F>
+// The columns k = 0..d-1 in order: k = 4 (j + L g) + e, owner lane j of the chain's L (runtime, wave-uniform),
+// owner slot 4 g + e (unrolled).  col(k, j, ks) is called once per column.
+template <int G, int L, class F>
 __device__ __forceinline__ void ram_wave_columns(int d, F&& col) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        for (int j = 0; j < 64; ++j) {
-            const int kb = 4 * (j + 64 * g);
+        for (int j = 0; j < L; ++j) {
+            const int kb = 4 * (j + L * g);
             if (kb >= d) return;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -173,31 +186,31 @@ __device__ __forceinline__ void ram_wave_columns(int d, F&& col) {
     }
 }
 
-// column k's entries of this lane's rows (q >= k, q < d; else 0)
-template <int NC>
+// column k's entries of this lane's rows (q >= k, q < d; else 0); lane: the lane within the chain's L
+template <int NC, int L>
 __device__ __forceinline__ void ram_wave_load_col(ram_rsrc_t S, uint32_t vo, int lane, int d, int k, double (&v)[NC]) {
     const int base = (int)(ram_wave_colstart(k, d) - k);
 #pragma unroll
     for (int s = 0; s < NC; ++s) {
-        const int q = 4 * (lane + 64 * (s >> 2)) + (s & 3);
-        v[s] = (q >= k && q < d) ? ram_wload(S, vo, (base + 256 * (s >> 2) + (s & 3)) * 8) : 0.0;
+        const int q = 4 * (lane + L * (s >> 2)) + (s & 3);
+        v[s] = (q >= k && q < d) ? ram_wload(S, vo, (base + 4 * L * (s >> 2) + (s & 3)) * 8) : 0.0;
     }
 }
 
 // u = S z (rows owned as above): per row the fma chain over c = 0..q, one column at a time
-template <int G>
+template <int G, int L>
 __device__ __forceinline__ void ram_wave_matvec(ram_rsrc_t S, uint32_t vo, int lane, int d, const double (&z)[4 * G],
                                                 double (&u)[4 * G]) {
     constexpr int NC = 4 * G;
 #pragma unroll
     for (int s = 0; s < NC; ++s) u[s] = 0.0;
-    ram_wave_columns<G>(d, [&](int k, int j, int ks) {
-        const double zk = ram_readlane(z[ks], j);
+    ram_wave_columns<G, L>(d, [&](int k, int j, int ks) {
+        const double zk = ram_bcast<L>(z[ks], j);
         double v[NC];
-        ram_wave_load_col<NC>(S, vo, lane, d, k, v);
+        ram_wave_load_col<NC, L>(S, vo, lane, d, k, v);
 #pragma unroll
         for (int s = 0; s < NC; ++s) {
-            const int q = 4 * (lane + 64 * (s >> 2)) + (s & 3);
+            const int q = 4 * (lane + L * (s >> 2)) + (s & 3);
             if (q >= k && q < d) u[s] = __builtin_fma(v[s], zk, u[s]);
         }
     });
@@ -205,7 +218,7 @@ __device__ __forceinline__ void ram_wave_matvec(ram_rsrc_t S, uint32_t vo, int l
 
 // ram_update for the wave layout (same operations per entry, same NEXT fold of the next step's S z, whose
 // normals zn are drawn beforehand)
-template <int G, bool NEXT>
+template <int G, int L, bool NEXT>
 __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, uint32_t vo, int lane, int d,
                                                 double alpha, double nz, double (&u)[4 * G],
                                                 const double (&zn)[4 * G], double (&un)[4 * G]) {
@@ -220,14 +233,14 @@ __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, ui
         for (int s = 0; s < NC; ++s) un[s] = 0.0;
     }
     double l0[NC];
-    ram_wave_load_col<NC>(Ss, vo, lane, d, 0, l0);
-    ram_wave_columns<G>(d, [&](int k, int j, int ks) {
+    ram_wave_load_col<NC, L>(Ss, vo, lane, d, 0, l0);
+    ram_wave_columns<G, L>(d, [&](int k, int j, int ks) {
         const int base = (int)(ram_wave_colstart(k, d) - k);
         double l1[NC];
-        if (k + 1 < d) ram_wave_load_col<NC>(Ss, vo, lane, d, k + 1, l1);
-        const double zk = NEXT ? ram_readlane(zn[ks], j) : 0.0;
-        const double lkk = ram_readlane(l0[ks], j);
-        const double xk = ram_readlane(u[ks], j);
+        if (k + 1 < d) ram_wave_load_col<NC, L>(Ss, vo, lane, d, k + 1, l1);
+        const double zk = NEXT ? ram_bcast<L>(zn[ks], j) : 0.0;
+        const double lkk = ram_bcast<L>(l0[ks], j);
+        const double xk = ram_bcast<L>(u[ks], j);
         const double t2 = xk * xk;
         const double l2 = lkk * lkk;
         const double r = __builtin_sqrt(up ? l2 + t2 : l2 - t2);
@@ -237,8 +250,8 @@ __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, ui
         const double ic = 1.0 / cc;
 #pragma unroll
         for (int s = 0; s < NC; ++s) {
-            const int q = 4 * (lane + 64 * (s >> 2)) + (s & 3);
-            const int so = (base + 256 * (s >> 2) + (s & 3)) * 8;
+            const int q = 4 * (lane + L * (s >> 2)) + (s & 3);
+            const int so = (base + 4 * L * (s >> 2) + (s & 3)) * 8;
             if (q == k) {
                 ram_wstore(Sd, vo, so, r);
                 if (NEXT) un[s] = __builtin_fma(r, zk, un[s]);

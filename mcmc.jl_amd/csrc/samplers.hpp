@@ -437,6 +437,95 @@ struct WaveChain {
     }
 };
 
+// Two chains per wave, 32 lanes per chain (RAM on separable targets, 32 < d <= 128 G; ram_wave_body): half h =
+// lane >> 5 of wave w runs chain 2 w + h, lane l = lane & 31 of it owns coordinates 4 (l + 32 k) + e; sums per lane,
+// then the butterfly over the half (oracle order ORC_ORDER_HALF).  The wave-uniform pivot work of a RAM column is
+// then shared by two chains.
+template <int G>
+struct HalfWaveChain {
+    static constexpr int NB = G;
+    static constexpr int NC = 4 * G;
+    static constexpr bool kPairs = false;
+    static constexpr int L = 32;
+    int64_t c;
+    bool live;
+    int d;
+    int lane;
+    int64_t ldr;
+    BmTables<kTabGlobal, kBlock> bt;
+    __device__ HalfWaveChain(const StepArgs& s) {
+        c = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 2 + ((threadIdx.x >> 5) & 1);
+        live = c < s.C;
+        d = s.d;
+        lane = (int)(threadIdx.x & 31);
+        ldr = s.ld;
+        bt.init();
+    }
+    __device__ __forceinline__ int coord(int k) const { return 4 * (lane + L * (k >> 2)) + (k & 3); }
+    __device__ __forceinline__ bool valid(int k) const { return coord(k) < d; }
+    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + L * b); }
+    __device__ __forceinline__ double reduce(double v) const {
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+        return v;
+    }
+    __device__ __forceinline__ bool any(bool v) const {
+        const uint64_t m = __ballot(v);
+        return ((threadIdx.x & 32) ? (m >> 32) : (m & 0xffffffffull)) != 0;
+    }
+    __device__ __forceinline__ void load(const double* x, int64_t /*ld*/, double (&v)[NC]) const {
+        const double* row = x + (size_t)(live ? c : 0) * (size_t)ldr;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = 4 * (lane + L * g);
+            if (j0 < d) {
+                const double4 q = *reinterpret_cast<const double4*>(row + j0);
+                v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+            } else {
+                v[4 * g] = v[4 * g + 1] = v[4 * g + 2] = v[4 * g + 3] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (!valid(k)) v[k] = 0.0;
+    }
+    __device__ __forceinline__ void store(double* x, int64_t /*ld*/, const double (&v)[NC]) const {
+        if (!live) return;
+        double* row = x + (size_t)c * (size_t)ldr;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = 4 * (lane + L * g);
+            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+        }
+    }
+    __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
+    template <class T>
+    __device__ __forceinline__ void store_t(T* p, T v) const {
+        if (live && lane == 0) p[c] = v;
+    }
+    // kept sample into the chain-major staging layout [nkept][C][ldr], as WaveChain
+    __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
+                                               double* base) const {
+        if (base == nullptr || !live) return;
+        double* row = base + ((size_t)kk * (size_t)s.C + (size_t)c) * (size_t)ldr;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int j0 = 4 * (lane + L * g);
+            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+        }
+    }
+    __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
+        if (s.n_evals != nullptr && live && lane == 0) atomicAdd(s.n_evals, (unsigned long long)n);
+    }
+    // the wave's two chains (2 w, 2 w + 1) are adjacent bits of one accept word: one atomicOr per wave
+    __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
+        const uint64_t m = __ballot(acc && live && lane == 0);
+        const uint64_t bits = (m & 1ull) | ((m >> 31) & 2ull);
+        if ((threadIdx.x & 63) == 0 && bits != 0 && s.acc_bits != nullptr)
+            atomicOr((unsigned long long*)&s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)(c >> 6)], bits << (c & 63));
+    }
+};
+
 // ------------------------------------------------------------------ shared pieces
 template <class P>
 __device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32_t chain, uint32_t step,
@@ -456,6 +545,7 @@ struct split_of<LaneChain<NB, F, S, T, TAB>> { static constexpr int value = Lane
 
 template <class P, class M>
 __device__ __forceinline__ double eval_lp(const P& p, const M& model, const double (&v)[P::NC], bool& oos) {
+    if constexpr (is_joint<M>::value) return model.joint_lp(v, oos);    // a joint target (lane per chain)
     constexpr int S = split_of<P>::value;
     if constexpr (S > 0) {                              // LaneChain SPLIT: PairChain's order (see LaneChain)
         double a = 0.0, b = 0.0;
@@ -473,6 +563,29 @@ __device__ __forceinline__ double eval_lp(const P& p, const M& model, const doub
         if (p.valid(k)) model.acc(a, v[k]);
     return llacc_finish(model, p.reduce(a), oos);
 }
+
+// The model's gradient at a point v, coordinate by coordinate: for a separable model the rule of coordinate k at
+// the use (g(k, v[k]) is model.grad(v[k]), the code as before); for a joint model (is_joint) the whole gradient,
+// formed once when need is set (a point out of support never reads it)
+template <class M, int NC, bool J = is_joint<M>::value>
+struct GradAt {
+    const M& m;
+    __device__ __forceinline__ GradAt(const M& model, const double (&)[NC], bool = true) : m(model) {}
+    __device__ __forceinline__ double operator()(int, double v) const { return m.grad(v); }
+};
+template <class M, int NC>
+struct GradAt<M, NC, true> {
+    double g[NC];
+    __device__ __forceinline__ GradAt(const M& model, const double (&v)[NC], bool need = true) {
+        if (need) {
+            model.joint_grad(v, g);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) g[k] = 0.0;
+        }
+    }
+    __device__ __forceinline__ double operator()(int k, double) const { return g[k]; }
+};
 
 template <class P>
 __device__ __forceinline__ double half_dot(const P& p, const double (&m)[P::NC]) {
@@ -630,9 +743,10 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
         double xp[P::NC];
         gen_normals(p, rs, chain, (uint32_t)i, xp);
         double qf = 0.0;
+        const GradAt<M, P::NC> gx(model, x);
 #pragma unroll
         for (int k = 0; k < P::NC; ++k) {
-            const double pm = x[k] + half * model.grad(x[k]);   // parsMean (MALA.jl:98)
+            const double pm = x[k] + half * gx(k, x[k]);        // parsMean (MALA.jl:98)
             xp[k] = pm + sq * xp[k];                            // MALA.jl:100
             const double e = pm - xp[k];
             if (p.valid(k)) qf = qf + ((-(e * e)) / twoh - L);  // MALA.jl:103
@@ -641,9 +755,10 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
         bool oos;
         const double lpp = eval_lp(p, model, xp, oos);
         double qb = 0.0;
+        const GradAt<M, P::NC> gxp(model, xp, !oos);
 #pragma unroll
         for (int k = 0; k < P::NC; ++k) {
-            const double gp = oos ? 0.0 : model.grad(xp[k]);
+            const double gp = oos ? 0.0 : gxp(k, xp[k]);
             const double e = (xp[k] + half * gp) - x[k];       // MALA.jl:104-105
             if (p.valid(k)) qb = qb + ((-(e * e)) / twoh - L);
         }
@@ -661,8 +776,9 @@ __device__ __forceinline__ void mala_body(const KernelArgs& a) {
             p.store_kept(s, kk, x, s.samples);
             if (s.grads != nullptr) {
                 double g[P::NC];
+                const GradAt<M, P::NC> gk(model, x);
 #pragma unroll
-                for (int k = 0; k < P::NC; ++k) g[k] = model.grad(x[k]);
+                for (int k = 0; k < P::NC; ++k) g[k] = gk(k, x[k]);
                 p.store_kept(s, kk, g, s.grads);
             }
             p.store_bit(s, kk, acc);
@@ -699,8 +815,9 @@ __device__ __forceinline__ double trajectory(const P& p, const M& model, double 
     double lpl = 0.0;
     double kick[kCarry ? P::NC : 1];
     if constexpr (kCarry) {
+        const GradAt<M, P::NC> g0(model, x);
 #pragma unroll
-        for (int k = 0; k < P::NC; ++k) kick[k] = (0.5 * model.grad(x[k])) * eps;
+        for (int k = 0; k < P::NC; ++k) kick[k] = (0.5 * g0(k, x[k])) * eps;
     }
     for (int64_t l = 0; l < nl; ++l) {
 #pragma unroll
@@ -712,9 +829,10 @@ __device__ __forceinline__ double trajectory(const P& p, const M& model, double 
             x[k] = x[k] + eps * m[k];                           // n.pars += ve * n.m
         }
         if (M::kLLAcc) lpl = eval_lp(p, model, x, oos);         // calc!(n, ll)
+        const GradAt<M, P::NC> gl(model, x, !oos);
 #pragma unroll
         for (int k = 0; k < P::NC; ++k) {
-            const double g = oos ? 0.0 : model.grad(x[k]);
+            const double g = oos ? 0.0 : gl(k, x[k]);
             const double a = (0.5 * g) * eps;
             if constexpr (kCarry) kick[k] = a;
             m[k] = m[k] + a;
@@ -834,8 +952,9 @@ __device__ __forceinline__ void hmc_body(const KernelArgs& a) {
             p.store_kept(s, kk, x0, s.samples);
             if (s.grads != nullptr) {
                 double g[P::NC];
+                const GradAt<M, P::NC> gk(model, x0);
 #pragma unroll
-                for (int k = 0; k < P::NC; ++k) g[k] = model.grad(x0[k]);
+                for (int k = 0; k < P::NC; ++k) g[k] = gk(k, x0[k]);
                 p.store_kept(s, kk, g, s.grads);
             }
             p.store_bit(s, kk, acc);
@@ -904,8 +1023,11 @@ __device__ __forceinline__ void hmc_record_body(const KernelArgs& a, const LeapR
     }
     gen_normals(p, rs, chain, (uint32_t)i, m);                       // state0.m = randn(model.size)
     double H = -lp + half_dot(p, m);                                 // update!(state0)
+    {
+        const GradAt<M, P::NC> g0(model, x);
 #pragma unroll
-    for (int k = 0; k < P::NC; ++k) g[k] = model.grad(x[k]);         // the state's gradient (in support)
+        for (int k = 0; k < P::NC; ++k) g[k] = g0(k, x[k]);          // the state's gradient (in support)
+    }
     const size_t C = (size_t)s.C;
     p.store_cm(s, 0, x, r.pars);                                     // leapStates[1] = deepcopy(state0)
     p.store_cm(s, 0, g, r.grads);
@@ -921,9 +1043,10 @@ __device__ __forceinline__ void hmc_record_body(const KernelArgs& a, const LeapR
             x[k] = x[k] + eps * m[k];                                 // n.pars += ve * n.m
         }
         const double lpl = eval_lp(p, model, x, oos);                // calc!(n, ll)
+        const GradAt<M, P::NC> gl(model, x, !oos);
 #pragma unroll
         for (int k = 0; k < P::NC; ++k) {
-            g[k] = oos ? 0.0 : model.grad(x[k]);
+            g[k] = oos ? 0.0 : gl(k, x[k]);
             m[k] = m[k] + (0.5 * g[k]) * eps;                         // n.m += 0.5*n.grad*ve
         }
         H = -lpl + half_dot(p, m);                                    // update!(n)
@@ -1059,17 +1182,22 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
     constexpr int NC = P::NC;
     constexpr int G = P::NB;
+    constexpr int L = P::L;               // lanes per chain: 64 (WaveChain) or 32 (HalfWaveChain, two chains a wave)
+    constexpr int CPW = 64 / L;
     const int d = s.d;
     double x[NC];
     p.load(a.st.x, s.ld, x);
     double lp = p.load_scalar(a.st.lp);
-    // the chain's factor block in each half (the chain index is wave-uniform)
+    // the factor blocks of the wave's chains in each half: chains CPW w .. CPW w + CPW - 1 are adjacent blocks (the
+    // runtime allocates round_up(C, 4) of them), one buffer resource over them, the half's block by vector offset
     const int64_t cu = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    double* const B0 = a.st.ram_L + (uint64_t)cu * (uint64_t)a.st.ram_ld;
-    const uint64_t hs = (uint64_t)a.st.ram_hs;
+    if (cu * CPW >= s.C) return;          // a tail wave with no live chain (no barriers below: it may leave)
     const int64_t ld = a.st.ram_ld;
-    const int lane = (int)(threadIdx.x & 63);
-    const uint32_t vo = (uint32_t)lane * 32;
+    double* const B0 = a.st.ram_L + (uint64_t)(cu * CPW) * (uint64_t)ld;
+    const uint64_t hs = (uint64_t)a.st.ram_hs;
+    const int64_t rbytes = ld * 8 * CPW;
+    const int lane = p.lane;
+    const uint32_t vo = (uint32_t)((threadIdx.x & 63) / L) * (uint32_t)(ld * 8) + (uint32_t)lane * 32;
     double u[NC], nz;
     if (s.nsteps > 0) {
         const int64_t i = s.step_begin;
@@ -1082,7 +1210,7 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
             a2 = __builtin_fma(z[k], z[k], a2);                               // dot(rvec, rvec)
         }
         nz = p.reduce(a2);
-        ram_wave_matvec<G>(ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld), vo, lane, d, z, u);
+        ram_wave_matvec<G, L>(ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, rbytes), vo, lane, d, z, u);
     }
     Keeper keep(s);
     for (int t = 0; t < s.nsteps; ++t) {
@@ -1108,8 +1236,8 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
             p.store_bit(s, kk, acc);
         }
         const double alpha = ram_alpha(i, d, ratio, sa.rate);
-        const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld);
-        const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, ld);
+        const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, rbytes);
+        const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, rbytes);
         if (t + 1 < s.nsteps) {
             double zn[NC], un[NC];
             gen_normals(p, rs, chain, (uint32_t)(i + 1), zn);                  // step i + 1's rvec
@@ -1119,13 +1247,13 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
                 if (!p.valid(k)) zn[k] = 0.0;
                 a2 = __builtin_fma(zn[k], zn[k], a2);
             }
-            ram_wave_update<G, true>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
+            ram_wave_update<G, L, true>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
 #pragma unroll
             for (int k = 0; k < NC; ++k) u[k] = un[k];
             nz = p.reduce(a2);
         } else {
             double zn[NC], un[NC];
-            ram_wave_update<G, false>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
+            ram_wave_update<G, L, false>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
         }
     }
     p.store(a.st.x, s.ld, x);
@@ -1148,8 +1276,9 @@ __device__ __forceinline__ void eval_body(const KernelArgs& a, const double* xin
     p.store_t(lp_out, lp);
     if (g_out != nullptr) {
         double g[P::NC];
+        const GradAt<M, P::NC> gx(model, x, !oos);
 #pragma unroll
-        for (int k = 0; k < P::NC; ++k) g[k] = oos ? 0.0 : model.grad(x[k]);
+        for (int k = 0; k < P::NC; ++k) g[k] = oos ? 0.0 : gx(k, x[k]);
         p.store(g_out, s.ld, g);
     }
     if (check && p.live && !(lp - lp == 0.0)) atomicOr(s.err, 1);

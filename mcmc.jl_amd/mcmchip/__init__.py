@@ -6,6 +6,7 @@ runs in the HIP kernels of libmcmc_hip.so through the C ABI (include/mcmc_hip.h)
 from ._lib import MCMCError, OutOfSupportError, load as load_library, LIB_PATH  # noqa: F401
 from .api import (  # noqa: F401
     IsoNormalDot, NormalDSL, AbsNormalDSL, DistDSL, DistObsDSL, LogisticRegression, LinearRegression, ProbitRegression, vaso_data,
+    OrnsteinUhlenbeck, ou_series,
     MCMCLikelihoodModel, model,
     RWM, MALA, HMC, HMCDA, RAM, EmpMCTuner, EmpiricalMCMCTuner, SerialMC, MCMCTask, MCMCChain,
     run, resume, device_count,

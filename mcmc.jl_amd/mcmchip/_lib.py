@@ -29,6 +29,7 @@ MODEL_ABS_NORMAL_DSL = 5
 MODEL_DIST_DSL = 6
 MODEL_PROBIT = 7
 MODEL_DIST_OBS = 8
+MODEL_OU = 9
 
 # MCMC_DIST_* (include/mcmc_hip.h)
 DISTS = {"Normal": 1, "Uniform": 2, "Weibull": 3, "Beta": 4, "TDist": 5, "Exponential": 6, "Gamma": 7,

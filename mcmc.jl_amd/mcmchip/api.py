@@ -30,7 +30,8 @@ from . import _lib
 from ._lib import check, dptr
 
 __all__ = [
-    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "DistObsDSL", "LogisticRegression", "LinearRegression", "ProbitRegression", "vaso_data", "MCMCLikelihoodModel", "model",
+    "IsoNormalDot", "NormalDSL", "AbsNormalDSL", "DistDSL", "DistObsDSL", "LogisticRegression", "LinearRegression", "ProbitRegression", "vaso_data",
+    "OrnsteinUhlenbeck", "ou_series", "MCMCLikelihoodModel", "model",
     "RWM", "MALA", "HMC", "HMCDA", "RAM", "EmpMCTuner", "EmpiricalMCMCTuner", "SerialMC", "MCMCTask", "MCMCChain",
     "run", "resume", "device_count",
 ]
@@ -152,6 +153,32 @@ class ProbitRegression:
         self.prior_sigma = float(prior_sigma)
 
 
+class OrnsteinUhlenbeck:
+    """examples/ornstein.jl:19-30: parameters (tau, sigma, mu) with tau ~ Uniform(0, 100), sigma ~ Uniform(0, 2),
+    mu ~ Uniform(0, 20); fac = exp(-1/tau); resid = x[2:end] - x[1:end-1]*fac - mu*(1-fac); resid ~ Normal(0, sigma),
+    over the series x.  The example: model(OrnsteinUhlenbeck(x), tau=0.05, sigma=1., mu=1., gradient=True) with
+    m.scale = [1000., 1., 10.] (ornstein.jl:29-30), run under RAM() and HMC(5, 0.002)."""
+    kind = _lib.MODEL_OU
+
+    def __init__(self, x):
+        self.series = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+        if self.series.shape[0] < 2:
+            raise ValueError("the Ornstein-Uhlenbeck model needs a series of at least 2 values")
+
+
+def ou_series(duration: int = 1000, mu0: float = 10.0, tau0: float = 20.0, sigma0: float = 0.1, seed: int = 1):
+    """The example's simulated series (examples/ornstein.jl:6-17): x[1] = 1, x[i] = x[i-1] exp(-1/tau0) +
+    mu0 (1 - exp(-1/tau0)) + sigma0 randn().  numpy's normal stream stands in for Julia's srand(1) randn, so the
+    values are the example's process, not its exact draws."""
+    rng = np.random.default_rng(seed)
+    x = np.empty(duration)
+    x[0] = 1.0
+    e = np.exp(-1.0 / tau0)
+    for i in range(1, duration):
+        x[i] = x[i - 1] * e + mu0 * (1.0 - e) + sigma0 * rng.standard_normal()
+    return x
+
+
 def vaso_data(path):
     """The probit example's design matrix (examples/probit_regression.jl:7-16): vaso.txt's covariates standardised
     (mean / sample std per column), polynomial order 1, a leading column of ones; the last column is y."""
@@ -215,6 +242,9 @@ class MCMCLikelihoodModel:
             desc.n = t.X.shape[0]
             desc.X = dptr(t.X)
             desc.Y = dptr(t.Y)
+        elif hasattr(t, "series"):
+            desc.n = t.series.shape[0]
+            desc.Y = dptr(t.series)
         return desc
 
     def eval(self, x, device: int = 0):

@@ -18,7 +18,9 @@
  * (order 0, lane-per-chain kernels) or per-lane partials + xor butterfly over 64
  * lanes (order 1, wave-per-chain kernels); order W > 1: a chain spread over W waves (lane l of 64 W owns
  * 4 (l + 64 W k) + e), each wave's butterfly, then the W wave sums left to right (block-per-chain kernels);
- * order ORC_ORDER_PAIR (-2): two lanes per chain (16 < d <= 32), each half left to right, then the halves added.
+ * order ORC_ORDER_PAIR (-2): two lanes per chain (16 < d <= 32), each half left to right, then the halves added;
+ * order ORC_ORDER_HALF (-3): two chains per wave, 32 lanes per chain (RAM steps on separable targets, 32 < d <= 256;
+ * their chains' initial log-targets come from the wave-per-chain eval kernel, order 1: orc_eval_order).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -35,6 +37,7 @@
 #define ORC_MODEL_DIST 6
 #define ORC_MODEL_PROBIT 7
 #define ORC_MODEL_DIST_OBS 8
+#define ORC_MODEL_OU 9
 
 #define ORC_RWM 1
 #define ORC_MALA 2
@@ -89,14 +92,20 @@ static const double ORC_TWOPI = 0x1.921fb54442d18p+2;
 /* order 1: lane l of a 64-lane wave owns coordinates 4*(l + 64k) + e, e = 0..3, k = 0,1,...;
    each lane accumulates its coordinates in (k, e) order, then xor butterfly 32,16,...,1.
    order W > 1: lane l of 64 W owns 4*(l + 64 W k) + e; butterfly per wave, wave sums left to right. */
-static double orc_butterfly(double p[64]) {
-    for (int off = 32; off >= 1; off >>= 1) {
+/* order ORC_ORDER_HALF (RAM on separable targets, 32 < d <= 256; samplers.hpp HalfWaveChain): two chains per wave,
+   lane l of a chain's 32 owns 4*(l + 32k) + e; per lane in (k, e) order, then xor butterfly 16,...,1. */
+#define ORC_ORDER_HALF (-3)
+static double orc_butterfly_n(double* p, int nl) {
+    for (int off = nl / 2; off >= 1; off >>= 1) {
         double q[64];
-        for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ off];
-        memcpy(p, q, sizeof q);
+        for (int l = 0; l < nl; ++l) q[l] = p[l] + p[l ^ off];
+        memcpy(p, q, sizeof(double) * (size_t)nl);
     }
     return p[0];
 }
+static double orc_butterfly(double p[64]) { return orc_butterfly_n(p, 64); }
+/* the eval kernel's order for a run's order (the initial log-target of SamplerTask / SeqMC particles) */
+static int orc_eval_order(int order) { return order == ORC_ORDER_HALF ? 1 : order; }
 
 typedef struct { int d_pad, nw, ds; int64_t n_pad; } orc_glm_geo;
 static orc_glm_geo orc_glm_geometry(const orc_model* m);
@@ -128,17 +137,18 @@ static double orc_dot(const double* v, const orc_model* mdl, int order) {
         for (int j = 0; j < d; ++j) a = fma(v[j], v[j], a);
         return a;
     }
-    const int W = order, L = 64 * order;          /* W waves per chain, lane l owns 4 (l + L k) + e */
+    const int half = order == ORC_ORDER_HALF;
+    const int W = half ? 1 : order, NL = half ? 32 : 64, L = NL * W;   /* W waves per chain, lane l owns 4 (l + L k) + e */
     double tot = 0.0;
     for (int w = 0; w < W; ++w) {
         double p[64];
-        for (int l = 0; l < 64; ++l) {
+        for (int l = 0; l < NL; ++l) {
             double a = 0.0;
-            for (int j0 = 4 * (64 * w + l); j0 < d; j0 += 4 * L)
+            for (int j0 = 4 * (NL * w + l); j0 < d; j0 += 4 * L)
                 for (int e = 0; e < 4 && j0 + e < d; ++e) a = fma(v[j0 + e], v[j0 + e], a);
             p[l] = a;
         }
-        const double sw = orc_butterfly(p);
+        const double sw = orc_butterfly_n(p, NL);
         tot = w == 0 ? sw : tot + sw;             /* waves left to right */
     }
     return tot;
@@ -162,17 +172,18 @@ static double orc_sum(const double* t, const orc_model* mdl, int order) {
         for (int j = 0; j < d; ++j) a = a + t[j];
         return a;
     }
-    const int W = order, L = 64 * order;
+    const int half = order == ORC_ORDER_HALF;
+    const int W = half ? 1 : order, NL = half ? 32 : 64, L = NL * W;
     double tot = 0.0;
     for (int w = 0; w < W; ++w) {
         double p[64];
-        for (int l = 0; l < 64; ++l) {
+        for (int l = 0; l < NL; ++l) {
             double a = 0.0;
-            for (int j0 = 4 * (64 * w + l); j0 < d; j0 += 4 * L)
+            for (int j0 = 4 * (NL * w + l); j0 < d; j0 += 4 * L)
                 for (int e = 0; e < 4 && j0 + e < d; ++e) a = a + t[j0 + e];
             p[l] = a;
         }
-        const double sw = orc_butterfly(p);
+        const double sw = orc_butterfly_n(p, NL);
         tot = w == 0 ? sw : tot + sw;
     }
     return tot;
@@ -381,6 +392,52 @@ static double orc_dist_grad(int dist, double p1, double p2, double v) {
 
 static double orc_eval(const orc_model* m, const double* x, double* g, double* tmp, int order) {
     const int d = m->d;
+    if (m->kind == ORC_MODEL_OU) {
+        /* examples/ornstein.jl:19-30 (models.hpp OUDSL): pars (tau, sigma, mu), series Y[0..n-1].  LLAcc(0.) +
+           logpdf(Uniform(0,100), tau) + logpdf(Uniform(0,2), sigma) + logpdf(Uniform(0,20), mu) (-log(b - a) inside,
+           -Inf outside: OutOfSupportError), then + sum(logpdf(Normal(0, sigma), resid)) left to right with
+           resid_i = (Y[i] - Y[i-1] fac) - mu (1 - fac), fac = exp(-1/tau).  Gradient by reverse mode with the DSL's
+           rules (MCMCDerivRules.jl:57-59 Normal dx / dsigma, :62 Uniform dx = 0): dr = (0 - r)/(sigma sigma),
+           d tau = (mu G0 - G1)(fac/(tau tau)), d sigma = sum ((r r)/(sigma sigma) - 1)/sigma, d mu = -(G0 (1 - fac)). */
+        const double tau = x[0], sigma = x[1], mu = x[2];
+        const int insup = tau >= 0.0 && tau <= 100.0 && sigma >= 0.0 && sigma <= 2.0 && mu >= 0.0 && mu <= 20.0;
+        double lp = -INFINITY;
+        int oos = 1;
+        if (insup) {
+            const double c0 = ((0.0 + -log(100.0)) + -log(2.0)) + -log(20.0);   /* host glibc, as the runtime */
+            const double fac = orc_exp(-1.0 / tau);
+            const double c = mu * (1.0 - fac);
+            const double logsig = orc_log(sigma);
+            double s = 0.0;
+            for (int64_t i = 1; i < m->n; ++i) {
+                const double z = ((m->Y[i] - m->Y[i - 1] * fac) - c) / sigma;
+                s = s + (-0.5 * (z * z + ORC_LOG2PI) - logsig);
+            }
+            lp = c0 + s;
+            oos = !isfinite(lp);
+            if (oos) lp = -INFINITY;
+        }
+        if (g) {
+            g[0] = g[1] = g[2] = 0.0;
+            if (!oos) {
+                const double fac = orc_exp(-1.0 / tau);
+                const double c = mu * (1.0 - fac);
+                const double s2 = sigma * sigma;
+                double g0 = 0.0, g1 = 0.0, gs = 0.0;
+                for (int64_t i = 1; i < m->n; ++i) {
+                    const double r = (m->Y[i] - m->Y[i - 1] * fac) - c;
+                    const double dr = (0.0 - r) / s2;
+                    g0 = g0 + dr;
+                    g1 = g1 + dr * m->Y[i - 1];
+                    gs = gs + ((r * r) / s2 - 1.0) / sigma;
+                }
+                g[0] = (mu * g0 - g1) * (fac / (tau * tau));
+                g[1] = gs;
+                g[2] = -(g0 * (1.0 - fac));
+            }
+        }
+        return lp;
+    }
     if (m->kind == ORC_MODEL_DIST_OBS) {
         /* benchmarks/benchunits/bare_distribs.jl:13: y = x * v; y ~ Dist(p1, p2), scalar x, data v = Y [n]: the LLAcc
            sum left to right, d/dx = sum_i v_i dlogpdf(x v_i) (left to right) */
@@ -759,7 +816,7 @@ int64_t orc_init(const orc_model* m, const orc_sampler* s, int64_t C, orc_state*
     double* tmp = buf + d;
     for (int64_t c = 0; c < C; ++c) {
         for (int j = 0; j < d; ++j) x[j] = st->x[(size_t)j * C + c];
-        double lp = orc_eval(m, x, NULL, tmp, order);
+        double lp = orc_eval(m, x, NULL, tmp, orc_eval_order(order));
         st->lp[c] = lp;
         if (!isfinite(lp)) bad++;
         const int tuned = s->tuner && (s->kind == ORC_MALA || s->kind == ORC_HMC);
@@ -999,7 +1056,7 @@ void orc_seqmc(const orc_model* const* models, const orc_sampler* const* sampler
                     st->x[(size_t)j * N + n] = pars[(size_t)j * N + n];
                     xv[j] = pars[(size_t)j * N + n];
                 }
-                st->lp[n] = orc_eval(m, xv, NULL, tmp, order);
+                st->lp[n] = orc_eval(m, xv, NULL, tmp, orc_eval_order(order));
                 ll0[n] = st->lp[n];
             }
             orc_run(m, samplers[t], seeds[t], 0, N, 0, N, steps_done[t], 0, 1, 1, st, NULL, NULL, NULL, order, 1);

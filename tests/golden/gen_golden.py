@@ -69,6 +69,7 @@ SAMPLERS = {
                               else mc.HMC(3, 0.9, mc.EmpMCTuner(0.7, adaptStep=5, maxStep=9))),
     "hmcda": lambda glm: mc.HMCDA(len=0.1 if glm else 0.8),
     "ram": lambda glm: mc.RAM(1.0, 0.3 if glm else 0.234),
+    "ram_wide": lambda glm: mc.RAM(0.15, 0.234),            # 33 <= d <= 256: two chains per wave
 }
 
 # (name, model spec, sampler, runner (steps, burnin, thinning), chains, seed)
@@ -85,6 +86,8 @@ for _s in ("rwm", "mala", "hmc", "hmcda"):
 # HMCDA adapts its step only while i < burnin (HMCDA.jl:133): give it a burnin to adapt over
 CASES = [(n, sp, s, (r[0], 15, r[2]) if s == "hmcda" else r, C, sd) for n, sp, s, r, C, sd in CASES]
 CASES.append(("iso32_rwm", dict(model="iso", d=32), "rwm", (40, 5, 3), 64, 108))          # metric shape, small
+CASES.append(("iso40_ram", dict(model="iso", d=40), "ram_wide", (30, 3, 3), 5, 109))   # two chains per wave, a dead half
+CASES.append(("gamma200_ram", dict(model="gamma", d=200), "ram_wide", (12, 2, 2), 3, 110))   # two slot groups per lane
 # the exact configurations the benchmarks run (uniform scale: the kernel instances bench.py dispatches),
 # at small chain counts that are not multiples of 64
 CASES.append(("readme_rwm", dict(model="readme", d=3), "rwm01", (1000, 100, 1), 1, 1))   # config 1: README.md:60,85

@@ -100,6 +100,10 @@ class OracleModel:
             s.n = self.X.shape[0]
             s.X = _d(self.X)
             s.Y = _d(self.Y)
+        elif getattr(t, "series", None) is not None:       # the OU model's series (MODEL_OU)
+            self.Y = t.series
+            s.n = self.Y.shape[0]
+            s.Y = _d(self.Y)
         s.scale = _d(self.scale)
         self.s = s
         self.size = m.size
@@ -114,6 +118,8 @@ def oracle_sampler(sp) -> OSampler:
 
 
 ORDER_PAIR = -2          # oracle.c ORC_ORDER_PAIR: two lanes per chain (16 < d <= 32)
+ORDER_HALF = -3          # oracle.c ORC_ORDER_HALF: two chains per wave (RAM steps on separable targets, 32 < d <= 256)
+RAM_HALF_MAX_D = 256     # samplers.hpp HalfWaveChain: the widest d the two-chains-per-wave RAM kernel runs
 
 
 def kernel_order(m, sampler_kind=None):
@@ -121,10 +127,13 @@ def kernel_order(m, sampler_kind=None):
     regression targets have their own fixed order (the oracle picks it from the model: 0 here); separable targets:
     lane per chain for d <= 16 (0), two lanes per chain for 16 < d <= 32 (ORDER_PAIR; RAM runs lane per chain there
     but sums its log-target in that order, its |z|^2 left to right), wave per chain up to 2048 (1), block per chain
-    of 4 / 8 waves up to 8192 / 16384."""
+    of 4 / 8 waves up to 8192 / 16384.  RAM for 32 < d <= 256 runs two chains per wave (ORDER_HALF; the chains'
+    initial log-targets still come from the eval kernel's order 1, oracle.c orc_eval_order)."""
     d = m.size
     if getattr(m.target, "X", None) is not None:         # logistic / linear regression
         return 0
+    if sampler_kind == 5 and 32 < d <= RAM_HALF_MAX_D:
+        return ORDER_HALF
     return 0 if d <= 16 else ORDER_PAIR if d <= 32 else 1 if d <= 2048 else 4 if d <= 8192 else 8
 
 
@@ -210,6 +219,8 @@ def seqmc(targets, particles, steps, burnin, trigger, seed, target_seeds, order=
     nt = len(chains)
     if order is None:
         order = chains[0].order
+        if any(c.order != order for c in chains):   # orc_seqmc takes one order for every target
+            raise NotImplementedError("oracle seqmc: targets whose kernels sum in different orders")
     models = (ct.POINTER(OModel) * nt)(*[ct.pointer(c.om.s) for c in chains])
     samplers = (ct.POINTER(OSampler) * nt)(*[ct.pointer(c.os) for c in chains])
     states = (ct.POINTER(OState) * nt)(*[ct.pointer(c.st) for c in chains])

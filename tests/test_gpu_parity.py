@@ -631,17 +631,19 @@ def test_ram_continue_spl_and_shards(gpu):
 
 
 @pytest.mark.parametrize("mkind", ["iso", "normal", "abs", "dist"])
-@pytest.mark.parametrize("d", [33, 64, 100, 256, 257, 513, 1024])
+@pytest.mark.parametrize("d", [33, 64, 100, 128, 129, 200, 256, 257, 513, 1024])
 def test_ram_wave_parity(gpu, mkind, d):
     """32 < d <= 1024 (RAM.jl:41-80 has no d cap): wave-per-chain RAM, the factor column-major per chain and its
     rows spread over the lanes; samples, accept bits, final state and every factor bit-identical to the oracle in
-    the wave order (d <= 256: one slot group per lane, 257..512: two, 513..1024: four; tail wave and tail block)."""
+    the kernel's order (d <= 256: two chains per wave, one / two slot groups per lane, ORDER_HALF, 7 chains so the
+    last wave has a dead half; 257..512: one chain per wave, two slot groups, 513..1024: four; tail wave and tail
+    block)."""
     m = _ram_model(mkind, d)
     C = 7
     r = mc.SerialMC(steps=14 if d <= 256 else 8, burnin=2, thinning=2)
     task = (m * mc.RAM(0.7, 0.3) * r).batch(C, seed=777 + d, steps_per_launch=5)
     chain = mc.run(task)
-    assert task.step_kernel.startswith("wpc_ram<")
+    assert task.step_kernel.startswith("wpc_ram2<" if d <= 256 else "wpc_ram<")
     oc = orc.OracleChains(m, mc.RAM(0.7, 0.3), nchains=C, seed=777 + d, order=order_for(d))
     s_ref, _, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, None, acc_ref, "ram")
@@ -759,3 +761,63 @@ def test_dist_obs_gradient_samplers_bitwise(gpu, sname, name, p):
     oc = orc.OracleChains(m, sp(), nchains=130, seed=4)
     s_ref, g_ref, acc_ref = oc.run(r)
     assert_parity(chain, s_ref, g_ref, acc_ref, sname)
+
+
+# ------------------------------------------------------------------ Ornstein-Uhlenbeck (examples/ornstein.jl:19-30)
+from test_oracle import _ou_model  # noqa: E402
+
+OU_SAMPLERS = {"rwm": lambda: mc.RWM(0.05), "mala": lambda: mc.MALA(1e-5), "hmc": lambda: mc.HMC(5, 0.002),
+               "hmc_tuned": lambda: mc.HMC(3, 0.002, mc.EmpMCTuner(0.7, adaptStep=5, maxStep=9)),
+               "hmcda": lambda: mc.HMCDA(len=0.01), "ram": lambda: mc.RAM()}
+
+
+@pytest.mark.parametrize("sname", list(OU_SAMPLERS))
+def test_ou_sampler_parity(gpu, sname):
+    """The OU target (a joint, non-separable log-target over (tau, sigma, mu) and a 1 000-point series) on every
+    sampler from the example's init and scale hint (ornstein.jl:29-30), 70 chains (a tail wave): samples,
+    gradients, accept bits, final state and evaluation counts bitwise against the oracle."""
+    m = _ou_model()
+    r = mc.SerialMC(steps=40, burnin=6, thinning=3)
+    task = (m * OU_SAMPLERS[sname]() * r).batch(70, seed=29)
+    chain = mc.run(task)
+    assert task.step_kernel.startswith("lpc_") and "OUDSL" in task.step_kernel
+    oc = orc.OracleChains(m, OU_SAMPLERS[sname](), nchains=70, seed=29)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, sname.split("_")[0])
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert task.evals == int(oc.n_evals.sum())
+    if sname == "ram":
+        _assert_ram_factor(task, oc, 3)
+
+
+def test_ou_example_runs_bitwise(gpu):
+    """ornstein.jl:33-38 as written: one chain, run(m * RAM() * SerialMC(1000:10000)) and run(m * HMC(5, 0.002) *
+    SerialMC(1000:10000)), bitwise against the oracle; RAM's chain recovers the simulating parameters."""
+    m = _ou_model()
+    r = mc.SerialMC(steps=10000, burnin=999)
+    for sp in (mc.RAM, lambda: mc.HMC(5, 0.002)):
+        chain = mc.run((m * sp() * r).batch(1, seed=1))
+        oc = orc.OracleChains(m, sp(), nchains=1, seed=1)
+        s_ref, g_ref, acc_ref = oc.run(r)
+        assert np.array_equal(chain._samples, s_ref)
+        assert np.array_equal(chain.diagnostics["accept"].T, acc_ref.astype(bool))
+    chain = mc.run((m * mc.RAM() * r).batch(1, seed=1))
+    tail = chain._samples[5000:, :, 0].mean(axis=0)
+    assert abs(tail[2] - 10.0) < 0.5 and abs(tail[0] - 20.0) < 8.0 and abs(tail[1] - 0.1) < 0.02, tail
+
+
+def test_ou_eval_and_limits(gpu):
+    """model.eval / evalallg of the OU target on a batch (inside and outside the supports) bitwise against the
+    oracle; a model with d != 3 or a series shorter than 2 is refused."""
+    m = _ou_model()
+    rng = np.random.default_rng(5)
+    B = np.hstack([np.array([[0.05, 20.0, 100.0, -1.0, 5.0], [1.0, 0.1, 2.0, 1.0, 2.5], [1.0, 10.0, 20.0, 1.0, 1.0]]),
+                   np.vstack([rng.uniform(0.5, 99, 60), rng.uniform(0.05, 2, 60), rng.uniform(0, 20, 60)])])
+    lp, g = m.evalallg(B)
+    lp_r, g_r = orc.eval_batch(m, B)
+    assert np.array_equal(lp, lp_r) and np.array_equal(g, g_r)
+    bad = mc.model(mc.OrnsteinUhlenbeck(mc.ou_series()), init=np.ones(4), gradient=True)
+    with pytest.raises(mc.MCMCError, match="3 parameters"):
+        bad.eval(np.ones(4))
+    with pytest.raises(ValueError):
+        mc.OrnsteinUhlenbeck([1.0])

@@ -334,6 +334,42 @@ def test_pair_order_is_the_two_halves(d):
     assert np.array_equal(orc.eval_batch(m_iso, x)[0], lp)           # the default is the library's order
 
 
+@pytest.mark.parametrize("d", [33, 70, 128, 129, 256])
+def test_half_wave_order_is_a_32_lane_butterfly(d):
+    """ORDER_HALF (RAM on separable targets, 32 < d <= 256, two chains per wave): lane l of the chain's 32 owns
+    coordinates 4 (l + 32 k) + e, an fma chain per lane in (k, e) order, then the xor butterfly 16, 8, 4, 2, 1 --
+    restated here lane by lane, bitwise; the default order of RAM at these widths, the other samplers keep order 1."""
+    x = np.random.default_rng(d).normal(size=(d, 3))
+    m_iso = mc.model(mc.IsoNormalDot(), init=np.ones(d), grad=True)
+    lp, _ = orc.eval_batch(m_iso, x, order=orc.ORDER_HALF)
+    for c in range(3):
+        p = []
+        for lane in range(32):
+            a = 0.0
+            for j0 in range(4 * lane, d, 128):
+                for e in range(4):
+                    if j0 + e < d:
+                        a = _fma(x[j0 + e, c], x[j0 + e, c], a)
+            p.append(a)
+        for off in (16, 8, 4, 2, 1):
+            p = [p[lane] + p[lane ^ off] for lane in range(32)]
+        assert lp[c] == -p[0]
+    assert orc.kernel_order(m_iso, 5) == orc.ORDER_HALF
+    assert orc.kernel_order(m_iso, 1) == 1 == orc.kernel_order(m_iso)
+
+
+def test_half_wave_ram_initial_lp_in_eval_order():
+    """RAM chains at 33 <= d <= 256 start from the eval kernel's log-target (order 1, oracle.c orc_eval_order):
+    a zero-step run leaves the oracle's lp equal to eval_batch in order 1."""
+    d = 90
+    x0 = np.random.default_rng(3).normal(size=d)
+    m = mc.model(mc.IsoNormalDot(), init=x0, grad=True)
+    oc = orc.OracleChains(m, mc.RAM(), nchains=3, seed=1)
+    assert oc.order == orc.ORDER_HALF
+    lp1, _ = orc.eval_batch(m, np.repeat(x0[:, None], 3, axis=1), order=1)
+    assert np.array_equal(oc.lp, lp1)
+
+
 def test_init_out_of_support_raises():
     m = mc.model(mc.NormalDSL(0.0, 1.0), v=np.zeros(2), gradient=True)
     with pytest.raises(AssertionError, match="out of model support"):
@@ -703,3 +739,79 @@ def test_dist_obs_eval_matches_scipy(name, p):
             if np.isfinite(lp1[0]):
                 fd = (lp1[0] - lp[j]) / h
                 assert abs(g[0, j] - fd) <= 2e-3 * max(1.0, abs(fd)), (name, p, xs[0, j], g[0, j], fd)
+
+
+# ------------------------------------------------------------------ Ornstein-Uhlenbeck (examples/ornstein.jl:19-30)
+def _ou_model(x=None, init=(0.05, 1.0, 1.0)):
+    x = mc.ou_series() if x is None else x
+    m = mc.model(mc.OrnsteinUhlenbeck(x), tau=init[0], sigma=init[1], mu=init[2], gradient=True)
+    m.scale = np.array([1000.0, 1.0, 10.0])                 # ornstein.jl:30
+    return m
+
+
+def _ou_reference(x, B):
+    """The example's formulas evaluated independently (numpy / scipy, vectorised): Uniform priors, the residual
+    vector, sum(logpdf(Normal(0, sigma), resid)); gradient by hand-derived calculus."""
+    out, grads = [], []
+    for tau, sigma, mu in B.T:
+        if not (0 <= tau <= 100 and 0 <= sigma <= 2 and 0 <= mu <= 20):
+            out.append(-np.inf)
+            grads.append(np.zeros(3))
+            continue
+        fac = np.exp(-1.0 / tau)
+        r = x[1:] - x[:-1] * fac - mu * (1 - fac)
+        out.append(-np.log(100) - np.log(2) - np.log(20) + stats.norm(0, sigma).logpdf(r).sum())
+        dr = -r / sigma ** 2
+        grads.append(np.array([np.sum(dr * (mu - x[:-1])) * fac / tau ** 2,
+                               np.sum((r ** 2 / sigma ** 2 - 1) / sigma),
+                               -np.sum(dr) * (1 - fac)]))
+    return np.array(out), np.array(grads).T
+
+
+def test_ou_eval_matches_reference_formula():
+    """The oracle's OU log-target and gradient against the example's formulas (ornstein.jl:19-27), at points inside
+    and outside the Uniform supports, including the example's init (0.05, 1, 1)."""
+    x = mc.ou_series()
+    m = _ou_model(x)
+    rng = np.random.default_rng(19)
+    B = np.column_stack([[0.05, 1.0, 1.0], [20.0, 0.1, 10.0], [100.0, 2.0, 20.0], [-1.0, 1.0, 1.0], [5.0, 2.5, 1.0],
+                         [5.0, 1.0, 21.0]])
+    B = np.hstack([B, np.vstack([rng.uniform(0.5, 99, 30), rng.uniform(0.05, 2, 30), rng.uniform(0, 20, 30)])])
+    lp, g = orc.eval_batch(m, B)
+    lr, gr = _ou_reference(x, B)
+    assert np.array_equal(np.isfinite(lp), np.isfinite(lr))
+    ok = np.isfinite(lr)
+    assert not ok[3] and not ok[4] and not ok[5] and ok[2]           # Uniform bounds are closed (a <= x <= b)
+    np.testing.assert_allclose(lp[ok], lr[ok], rtol=1e-12)
+    np.testing.assert_allclose(g[:, ok], gr[:, ok], rtol=1e-9, atol=1e-9)
+    assert np.all(g[:, ~ok] == 0.0)                                  # LLAcc: (-Inf, zero gradient)
+
+
+def test_ou_gradient_finite_difference():
+    """helper_diff.jl:8-37's check on the OU target, away from the support edges."""
+    m = _ou_model()
+    x0 = np.array([[18.0], [0.12], [9.5]])
+    lp0, g0 = orc.eval_batch(m, x0)
+    for j, h in enumerate((1e-5, 1e-8, 1e-7)):
+        x1 = x0.copy()
+        x1[j] += h
+        gn = (orc.eval_batch(m, x1)[0] - lp0) / h
+        assert abs(g0[j, 0] - gn[0]) / max(1.0, abs(g0[j, 0])) < 2e-3
+
+
+def test_ou_example_posterior_ram():
+    """ornstein.jl:33-34: run(m * RAM() * SerialMC(1000:10000)) from the example's init and scale hint, here on 8
+    oracle chains: the posterior recovers the simulating parameters (mu0 = 10, tau0 = 20, sigma0 = 0.1)."""
+    m = _ou_model()
+    oc = orc.OracleChains(m, mc.RAM(), nchains=8, seed=34)
+    s, _, acc = oc.run(mc.SerialMC(steps=10000, burnin=999, thinning=10))
+    tail = s[len(s) // 2:]
+    tau, sigma, mu = (tail[:, j, :].mean() for j in range(3))
+    assert abs(mu - 10.0) < 0.5 and abs(tau - 20.0) < 6.0 and abs(sigma - 0.1) < 0.01, (tau, sigma, mu)
+    assert 0.05 < acc[len(acc) // 2:].mean() < 0.6
+
+
+def test_ou_init_out_of_support():
+    m = _ou_model(init=(-1.0, 1.0, 1.0))
+    with pytest.raises(AssertionError, match="out of model support"):
+        orc.OracleChains(m, mc.RAM(), nchains=2, seed=1)
