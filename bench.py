@@ -169,11 +169,15 @@ def measured_traffic(wkey, kname):
 
 def step_kernel_src_hash():
     """sha256 over the sources the lane- and wave-per-chain step kernels are compiled from (csrc/*.hpp, the
-    Box-Muller tables, kernels/lpc*, kernels/wpc*): a VALU profile recorded under another hash measured other code."""
+    Box-Muller tables, kernels/lpc*, kernels/wpc*): a VALU profile recorded under another hash measured other code.
+    ram.hpp / ram_wave.hpp (the RAM jump-factor templates and the wave-per-chain RAM body) and glm_layout.hpp (the
+    regression X image) are left out: no RWM / MALA / HMC step kernel instantiates them."""
     import glob
     import hashlib
     base = os.path.join(ROOT, "mcmc.jl_amd", "csrc")
-    files = sorted(glob.glob(os.path.join(base, "*.hpp")) + glob.glob(os.path.join(base, "*.inc"))
+    skip = {"ram.hpp", "ram_wave.hpp", "glm_layout.hpp"}
+    files = sorted([f for f in glob.glob(os.path.join(base, "*.hpp")) if os.path.basename(f) not in skip]
+                   + glob.glob(os.path.join(base, "*.inc"))
                    + glob.glob(os.path.join(base, "kernels", "lpc*")) + glob.glob(os.path.join(base, "kernels", "wpc*"))
                    + [os.path.join(base, "kernels", "layout_api.hpp")])
     h = hashlib.sha256()

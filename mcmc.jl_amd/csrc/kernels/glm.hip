@@ -1745,10 +1745,10 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
 // 128 < d <= 512: d-slices of 64 coordinates (NM = 4; the default, which the oracle restates) or, with
 // MCMCHIP_GLM_SLICE=128 (a dev A/B switch for benches only), of 128 (NM = 8, two 16-chain tiles per workgroup:
 // that build spills the HMC / MALA state at the 256-register budget, r04 measurements in DESIGN.md §5.3)
-static bool glm_narrow_slices() {
-    static const bool v = [] {
+static int glm_slice_override() {
+    static const int v = [] {
         const char* e = getenv("MCMCHIP_GLM_SLICE");
-        return !(e != nullptr && atoi(e) == 128);
+        return e != nullptr ? atoi(e) : 0;
     }();
     return v;
 }
@@ -1756,17 +1756,21 @@ static bool glm_narrow_slices() {
 mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
     // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1), 4 tiles
     // per workgroup;
-    // 128 < d <= 512: NW = d_pad / 64 slices (4 or 8) of DS = 64 coordinates (NM = 4), 8 / NW tiles of 16 chains
-    // per 8-wave workgroup (glm_narrow_slices);
+    // 128 < d <= 256: NW = 4 slices of DS = 64 coordinates (NM = 4), two 16-chain tiles per 8-wave workgroup;
+    // 256 < d <= 512: NW = 4 slices of DS = 128 (NM = 8), two tiles per workgroup, so each staged X tile feeds 32
+    // chains (round 4: config 5 0.557 -> 0.582 of the fp64 MFMA spec against 64-wide slices on one box; at d = 256
+    // 128-wide slices measured 0.30 against 0.53, two waves a tile);
     // 512 < d <= 1024: NW = 8 slices of DS = 128 coordinates (NM = 8), one tile per workgroup; d_pad = 1024 keeps
     // one LDS tile buffer (glm_xbufs).
+    // MCMCHIP_GLM_SLICE=64 / 128 forces the slice width for 128 < d <= 512 (bench A/B only: the oracle restates the
+    // default shapes).
     mcmc::GlmShape g{};
     if (d <= 128) {
         int nm = 1;
         while (16 * nm < d) nm *= 2;
         g.nw = 1;
         g.nm = nm;
-    } else if (d <= 512 && glm_narrow_slices()) {
+    } else if (glm_slice_override() == 64 ? d <= 512 : (d <= 256 && glm_slice_override() != 128)) {
         int nw = 4;
         while (64 * nw < d) nw *= 2;
         g.nw = nw;

@@ -1,7 +1,8 @@
 // wpc_ram.hip -- wave-per-chain RAM kernels (src/samplers/RAM.jl:41-79) for 32 < d <= 1024, every separable
-// model kind: samplers.hpp ram_wave_body over the ram.hpp wave layout of the jump factor (two chains per wave up to
-// d = 256, one beyond).
+// model kind: ram_wave.hpp ram_wave_body over the wave layout of the jump factor (two chains per wave up to d = 256,
+// one beyond).
 #include "wpc_impl.hpp"
+#include "../ram_wave.hpp"
 
 namespace mcmc {
 

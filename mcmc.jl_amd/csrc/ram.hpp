@@ -1,5 +1,6 @@
 // ram.hpp -- the jump-factor arithmetic of the robust adaptive Metropolis sampler (RAM.jl:55-78),
-// shared by the lane-per-chain (samplers.hpp ram_body) and regression (glm.hip glm_ram) kernels.
+// shared by the lane-per-chain (samplers.hpp ram_body) and regression (glm.hip glm_ram) kernels; the wave-per-chain
+// layout is ram_wave.hpp.
 //
 // Storage.  S is the chain's d x d lower-triangular jump factor, kept in HBM as packed rows padded to
 // the kernel's compile-time width DF >= d: element (r, c), c <= r < DF, is row idx = r(r+1)/2 + c.  The
@@ -126,145 +127,6 @@ __device__ __forceinline__ void ram_update(ram_rsrc_t Ss, ram_rsrc_t Sd, uint32_
         for (int q = k + 1; q < DF; ++q) l0[q] = l1[q];
         __builtin_amdgcn_sched_barrier(0);     // one column at a time
     }
-}
-
-// ------------------------------------------------------------------ wave-per-chain (32 < d <= 1024)
-// Storage.  One chain's factor is a block of ram_ld doubles (d(d+1)/2 rounded up to 8), column-major packed:
-// column k holds rows k..d-1 from ram_wave_colstart(k) = k d - k(k-1)/2, so element (q, k) is at
-// ram_wave_colstart(k) + q - k.  Blocks are chain-major ([chain][ram_ld]), the second half ram_hs doubles on.
-// The lanes own the rows that are their coordinates (WaveChain: lane l, slot s = 4g + e holds row
-// 4 (l + 64 g) + e), so a column's entries are one contiguous run the wave reads and writes together, through a
-// buffer resource over the chain's block: vector offset 32 l, scalar offset (colstart(k) - k + 256 g + e) 8.
-// Column k's pivot u[k] and S[k][k] come from their owner lane by readlane (k is wave-uniform); the next
-// column's entries are loaded while this one is computed.  (A straight-line variant that sends the lanes
-// outside the column to per-lane trash doubles instead of masking them measured 10% slower at d = 256.)
-__host__ __device__ constexpr int64_t ram_wave_colstart(int64_t k, int64_t d) { return k * d - k * (k - 1) / 2; }
-
-__device__ __forceinline__ double ram_readlane(double v, int l) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-
-// the factor blocks of a wave's chains (one block, or the two adjacent blocks of a HalfWaveChain pair)
-__device__ __forceinline__ ram_rsrc_t ram_chain_rsrc(const double* block, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(block), (short)0, (int)bytes, 0x00020000);
-}
-
-// column k's pivot entries from their owner lane j of each chain: one chain per wave (L = 64) reads lane j; two
-// chains per wave (L = 32) read lanes j and 32 + j and each half takes its own
-template <int L>
-__device__ __forceinline__ double ram_bcast(double v, int j) {
-    if constexpr (L == 64) {
-        return ram_readlane(v, j);
-    } else {
-        const double a = ram_readlane(v, j), b = ram_readlane(v, j + 32);
-        return (threadIdx.x & 32) ? b : a;
-    }
-}
-__device__ __forceinline__ double ram_wload(ram_rsrc_t r, uint32_t vo, int so) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
-}
-__device__ __forceinline__ void ram_wstore(ram_rsrc_t r, uint32_t vo, int so, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ram_u32x2, v), r, vo, so, 0);
-}
-
-// The columns k = 0..d-1 in order: k = 4 (j + L g) + e, owner lane j of the chain's L (runtime, wave-uniform),
-// owner slot 4 g + e (unrolled).  col(k, j, ks) is called once per column.
-template <int G, int L, class F>
-__device__ __forceinline__ void ram_wave_columns(int d, F&& col) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        for (int j = 0; j < L; ++j) {
-            const int kb = 4 * (j + L * g);
-            if (kb >= d) return;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (kb + e < d) col(kb + e, j, 4 * g + e);
-        }
-    }
-}
-
-// column k's entries of this lane's rows (q >= k, q < d; else 0); lane: the lane within the chain's L
-template <int NC, int L>
-__device__ __forceinline__ void ram_wave_load_col(ram_rsrc_t S, uint32_t vo, int lane, int d, int k, double (&v)[NC]) {
-    const int base = (int)(ram_wave_colstart(k, d) - k);
-#pragma unroll
-    for (int s = 0; s < NC; ++s) {
-        const int q = 4 * (lane + L * (s >> 2)) + (s & 3);
-        v[s] = (q >= k && q < d) ? ram_wload(S, vo, (base + 4 * L * (s >> 2) + (s & 3)) * 8) : 0.0;
-    }
-}
-
-// u = S z (rows owned as above): per row the fma chain over c = 0..q, one column at a time
-template <int G, int L>
-__device__ __forceinline__ void ram_wave_matvec(ram_rsrc_t S, uint32_t vo, int lane, int d, const double (&z)[4 * G],
-                                                double (&u)[4 * G]) {
-    constexpr int NC = 4 * G;
-#pragma unroll
-    for (int s = 0; s < NC; ++s) u[s] = 0.0;
-    ram_wave_columns<G, L>(d, [&](int k, int j, int ks) {
-        const double zk = ram_bcast<L>(z[ks], j);
-        double v[NC];
-        ram_wave_load_col<NC, L>(S, vo, lane, d, k, v);
-#pragma unroll
-        for (int s = 0; s < NC; ++s) {
-            const int q = 4 * (lane + L * (s >> 2)) + (s & 3);
-            if (q >= k && q < d) u[s] = __builtin_fma(v[s], zk, u[s]);
-        }
-    });
-}
-
-// ram_update for the wave layout (same operations per entry, same NEXT fold of the next step's S z, whose
-// normals zn are drawn beforehand)
-template <int G, int L, bool NEXT>
-__device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, uint32_t vo, int lane, int d,
-                                                double alpha, double nz, double (&u)[4 * G],
-                                                const double (&zn)[4 * G], double (&un)[4 * G]) {
-    constexpr int NC = 4 * G;
-    const double beta = alpha / nz;
-    const bool up = beta >= 0.0;
-    const double sb = __builtin_sqrt(__builtin_fabs(beta));
-#pragma unroll
-    for (int s = 0; s < NC; ++s) u[s] = sb * u[s];
-    if (NEXT) {
-#pragma unroll
-        for (int s = 0; s < NC; ++s) un[s] = 0.0;
-    }
-    double l0[NC];
-    ram_wave_load_col<NC, L>(Ss, vo, lane, d, 0, l0);
-    ram_wave_columns<G, L>(d, [&](int k, int j, int ks) {
-        const int base = (int)(ram_wave_colstart(k, d) - k);
-        double l1[NC];
-        if (k + 1 < d) ram_wave_load_col<NC, L>(Ss, vo, lane, d, k + 1, l1);
-        const double zk = NEXT ? ram_bcast<L>(zn[ks], j) : 0.0;
-        const double lkk = ram_bcast<L>(l0[ks], j);
-        const double xk = ram_bcast<L>(u[ks], j);
-        const double t2 = xk * xk;
-        const double l2 = lkk * lkk;
-        const double r = __builtin_sqrt(up ? l2 + t2 : l2 - t2);
-        const double cc = r / lkk;
-        const double sn = xk / lkk;
-        const double sns = up ? sn : -sn;
-        const double ic = 1.0 / cc;
-#pragma unroll
-        for (int s = 0; s < NC; ++s) {
-            const int q = 4 * (lane + L * (s >> 2)) + (s & 3);
-            const int so = (base + 4 * L * (s >> 2) + (s & 3)) * 8;
-            if (q == k) {
-                ram_wstore(Sd, vo, so, r);
-                if (NEXT) un[s] = __builtin_fma(r, zk, un[s]);
-            } else if (q > k && q < d) {
-                const double l = (l0[s] + sns * u[s]) * ic;
-                ram_wstore(Sd, vo, so, l);
-                u[s] = cc * u[s] - sn * l;
-                if (NEXT) un[s] = __builtin_fma(l, zk, un[s]);
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < NC; ++s) l0[s] = l1[s];
-    });
 }
 
 }  // namespace mcmc

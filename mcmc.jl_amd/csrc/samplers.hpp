@@ -437,95 +437,6 @@ struct WaveChain {
     }
 };
 
-// Two chains per wave, 32 lanes per chain (RAM on separable targets, 32 < d <= 128 G; ram_wave_body): half h =
-// lane >> 5 of wave w runs chain 2 w + h, lane l = lane & 31 of it owns coordinates 4 (l + 32 k) + e; sums per lane,
-// then the butterfly over the half (oracle order ORC_ORDER_HALF).  The wave-uniform pivot work of a RAM column is
-// then shared by two chains.
-template <int G>
-struct HalfWaveChain {
-    static constexpr int NB = G;
-    static constexpr int NC = 4 * G;
-    static constexpr bool kPairs = false;
-    static constexpr int L = 32;
-    int64_t c;
-    bool live;
-    int d;
-    int lane;
-    int64_t ldr;
-    BmTables<kTabGlobal, kBlock> bt;
-    __device__ HalfWaveChain(const StepArgs& s) {
-        c = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 2 + ((threadIdx.x >> 5) & 1);
-        live = c < s.C;
-        d = s.d;
-        lane = (int)(threadIdx.x & 31);
-        ldr = s.ld;
-        bt.init();
-    }
-    __device__ __forceinline__ int coord(int k) const { return 4 * (lane + L * (k >> 2)) + (k & 3); }
-    __device__ __forceinline__ bool valid(int k) const { return coord(k) < d; }
-    __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(lane + L * b); }
-    __device__ __forceinline__ double reduce(double v) const {
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-        return v;
-    }
-    __device__ __forceinline__ bool any(bool v) const {
-        const uint64_t m = __ballot(v);
-        return ((threadIdx.x & 32) ? (m >> 32) : (m & 0xffffffffull)) != 0;
-    }
-    __device__ __forceinline__ void load(const double* x, int64_t /*ld*/, double (&v)[NC]) const {
-        const double* row = x + (size_t)(live ? c : 0) * (size_t)ldr;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int j0 = 4 * (lane + L * g);
-            if (j0 < d) {
-                const double4 q = *reinterpret_cast<const double4*>(row + j0);
-                v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
-            } else {
-                v[4 * g] = v[4 * g + 1] = v[4 * g + 2] = v[4 * g + 3] = 0.0;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NC; ++k)
-            if (!valid(k)) v[k] = 0.0;
-    }
-    __device__ __forceinline__ void store(double* x, int64_t /*ld*/, const double (&v)[NC]) const {
-        if (!live) return;
-        double* row = x + (size_t)c * (size_t)ldr;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int j0 = 4 * (lane + L * g);
-            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
-        }
-    }
-    __device__ __forceinline__ double load_scalar(const double* p) const { return p[live ? c : 0]; }
-    template <class T>
-    __device__ __forceinline__ void store_t(T* p, T v) const {
-        if (live && lane == 0) p[c] = v;
-    }
-    // kept sample into the chain-major staging layout [nkept][C][ldr], as WaveChain
-    __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
-                                               double* base) const {
-        if (base == nullptr || !live) return;
-        double* row = base + ((size_t)kk * (size_t)s.C + (size_t)c) * (size_t)ldr;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int j0 = 4 * (lane + L * g);
-            if (j0 < d) *reinterpret_cast<double4*>(row + j0) = make_double4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
-        }
-    }
-    __device__ __forceinline__ void count_evals(const StepArgs& s, int64_t n) const {
-        if (s.n_evals != nullptr && live && lane == 0) atomicAdd(s.n_evals, (unsigned long long)n);
-    }
-    // the wave's two chains (2 w, 2 w + 1) are adjacent bits of one accept word: one atomicOr per wave
-    __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
-        const uint64_t m = __ballot(acc && live && lane == 0);
-        const uint64_t bits = (m & 1ull) | ((m >> 31) & 2ull);
-        if ((threadIdx.x & 63) == 0 && bits != 0 && s.acc_bits != nullptr)
-            atomicOr((unsigned long long*)&s.acc_bits[(size_t)kk * (size_t)s.nw + (size_t)(c >> 6)], bits << (c & 63));
-    }
-};
-
 // ------------------------------------------------------------------ shared pieces
 template <class P>
 __device__ __forceinline__ void gen_normals(const P& p, const Stream& rs, uint32_t chain, uint32_t step,
@@ -1163,97 +1074,6 @@ __device__ __forceinline__ void ram_body(const KernelArgs& a) {
             nz = nzn;
         } else {
             ram_update<NC, false>(Ss, Sd, vo, alpha, nz, u, zblock, un);
-        }
-    }
-    p.store(a.st.x, s.ld, x);
-    p.store_t(a.st.lp, lp);
-    p.count_evals(s, s.nsteps);
-}
-
-// Robust adaptive Metropolis for 32 < d <= 1024, wave per chain (ram.hpp wave layout): the lane-per-chain
-// body's steps with the factor's rows spread over the wave's lanes.
-template <class P, class M>
-__device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
-    const StepArgs& s = a.s;
-    const SamplerArgs& sa = a.sa;
-    const P p(s);
-    const M model(a.m);
-    const Stream rs{s.key0, s.key1};
-    const uint32_t chain = s.chain0 + (uint32_t)p.c;
-    constexpr int NC = P::NC;
-    constexpr int G = P::NB;
-    constexpr int L = P::L;               // lanes per chain: 64 (WaveChain) or 32 (HalfWaveChain, two chains a wave)
-    constexpr int CPW = 64 / L;
-    const int d = s.d;
-    double x[NC];
-    p.load(a.st.x, s.ld, x);
-    double lp = p.load_scalar(a.st.lp);
-    // the factor blocks of the wave's chains in each half: chains CPW w .. CPW w + CPW - 1 are adjacent blocks (the
-    // runtime allocates round_up(C, 4) of them), one buffer resource over them, the half's block by vector offset
-    const int64_t cu = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (cu * CPW >= s.C) return;          // a tail wave with no live chain (no barriers below: it may leave)
-    const int64_t ld = a.st.ram_ld;
-    double* const B0 = a.st.ram_L + (uint64_t)(cu * CPW) * (uint64_t)ld;
-    const uint64_t hs = (uint64_t)a.st.ram_hs;
-    const int64_t rbytes = ld * 8 * CPW;
-    const int lane = p.lane;
-    const uint32_t vo = (uint32_t)((threadIdx.x & 63) / L) * (uint32_t)(ld * 8) + (uint32_t)lane * 32;
-    double u[NC], nz;
-    if (s.nsteps > 0) {
-        const int64_t i = s.step_begin;
-        double z[NC];
-        gen_normals(p, rs, chain, (uint32_t)i, z);
-        double a2 = 0.0;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-            if (!p.valid(k)) z[k] = 0.0;
-            a2 = __builtin_fma(z[k], z[k], a2);                               // dot(rvec, rvec)
-        }
-        nz = p.reduce(a2);
-        ram_wave_matvec<G, L>(ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, rbytes), vo, lane, d, z, u);
-    }
-    Keeper keep(s);
-    for (int t = 0; t < s.nsteps; ++t) {
-        const int64_t i = s.step_begin + t;
-        double lpp;
-        {
-            double xp[NC];
-#pragma unroll
-            for (int k = 0; k < NC; ++k) xp[k] = x[k] + u[k];                 // RAM.jl:60
-            bool oos;
-            lpp = eval_lp(p, model, xp, oos);
-        }
-        const double ratio = lpp - lp;
-        const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
-        if (acc) {
-#pragma unroll
-            for (int k = 0; k < NC; ++k) x[k] = x[k] + u[k];
-            lp = lpp;
-        }
-        int64_t kk;
-        if (keep.take(i, &kk)) {
-            p.store_kept(s, kk, x, s.samples);
-            p.store_bit(s, kk, acc);
-        }
-        const double alpha = ram_alpha(i, d, ratio, sa.rate);
-        const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, rbytes);
-        const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, rbytes);
-        if (t + 1 < s.nsteps) {
-            double zn[NC], un[NC];
-            gen_normals(p, rs, chain, (uint32_t)(i + 1), zn);                  // step i + 1's rvec
-            double a2 = 0.0;
-#pragma unroll
-            for (int k = 0; k < NC; ++k) {
-                if (!p.valid(k)) zn[k] = 0.0;
-                a2 = __builtin_fma(zn[k], zn[k], a2);
-            }
-            ram_wave_update<G, L, true>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
-#pragma unroll
-            for (int k = 0; k < NC; ++k) u[k] = un[k];
-            nz = p.reduce(a2);
-        } else {
-            double zn[NC], un[NC];
-            ram_wave_update<G, L, false>(Ss, Sd, vo, lane, d, alpha, nz, u, zn, un);
         }
     }
     p.store(a.st.x, s.ld, x);

@@ -24,7 +24,7 @@ mutable struct Outputs             # mcmc_outputs (mutable: the library writes r
 end
 
 const MODEL_ISO_NORMAL_DOT, MODEL_NORMAL_DSL, MODEL_LOGISTIC, MODEL_LINEAR = 1, 2, 3, 4
-const MODEL_ABS_NORMAL_DSL, MODEL_DIST_DSL, MODEL_PROBIT, MODEL_DIST_OBS = 5, 6, 7, 8
+const MODEL_ABS_NORMAL_DSL, MODEL_DIST_DSL, MODEL_PROBIT, MODEL_DIST_OBS, MODEL_OU = 5, 6, 7, 8, 9
 const RWM_K, MALA_K, HMC_K, HMCDA_K, RAM_K = 1, 2, 3, 4, 5
 
 check(st) = st == 0 ? nothing :

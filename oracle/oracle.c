@@ -191,21 +191,21 @@ static double orc_sum(const double* t, const orc_model* mdl, int order) {
 
 /* ------------------------------------------------------------ regression models (MFMA kernels) */
 /* Geometry of the regression kernels (glm.hip mcmc_glm_shape): d <= 128: one wave per 16-chain tile with
-   DS = d_pad = 16 NM (NM a power of two); 128 < d <= 512: NW = 4 or 8 d-slices of DS = 64 coordinates (NM = 4),
-   d_pad = 64 NW; 512 < d <= 1024: NW = 8 d-slices of DS = 128 (NM = 8), d_pad = 1024; n_pad = round_up(n,16).
+   DS = d_pad = 16 NM (NM a power of two); 128 < d <= 256: NW = 4 d-slices of DS = 64 coordinates (NM = 4),
+   d_pad = 256; 256 < d <= 1024: NW = 4 or 8 d-slices of DS = 128 (NM = 8), d_pad = 128 NW; n_pad = round_up(n,16).
    Lane quarter q of the wave for slice s owns coordinates k = s*DS + 16m + 4q + e (m < DS/16, e < 4). */
 static orc_glm_geo orc_glm_geometry(const orc_model* m) {
     orc_glm_geo g;
     int nm = 1, nw = 1;
     if (m->d <= 128) {                    /* one slice: glm.hip glm_eval1 */
         while (16 * nm < m->d) nm *= 2;
-    } else if (m->d <= 512) {             /* d-slices of 64: glm_eval */
+    } else if (m->d <= 256) {             /* 4 d-slices of 64: glm_eval */
         nm = 4;
         nw = 4;
-        while (64 * nw < m->d) nw *= 2;
-    } else {                              /* 512 < d <= 1024: 8 d-slices of 128 (glm_eval, one tile buffer) */
+    } else {                              /* 256 < d <= 1024: 4 or 8 d-slices of 128 (glm_eval) */
         nm = 8;
-        nw = 8;
+        nw = 4;
+        while (128 * nw < m->d) nw *= 2;
     }
     g.ds = 16 * nm;
     g.nw = nw;

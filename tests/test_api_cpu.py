@@ -34,6 +34,21 @@ def test_library_exports_every_header_symbol():
     assert lib.mcmc_abi_version() == 1
 
 
+def test_model_kinds_agree_across_header_python_and_julia():
+    """MCMC_MODEL_* of include/mcmc_hip.h == mcmchip._lib.MODEL_* == MCMCHip.jl's MODEL_* constants."""
+    src = open(os.path.join(ROOT, "include", "mcmc_hip.h")).read()
+    hdr = {k: int(v) for k, v in re.findall(r"MCMC_MODEL_(\w+)\s*=\s*(\d+)", src)}
+    assert len(hdr) == 9 and hdr["OU"] == 9
+    jl = open(os.path.join(ROOT, "mcmc.jl_amd", "julia", "MCMCHip.jl")).read()
+    jlc = {}
+    for names, vals in re.findall(r"^const ((?:MODEL_\w+,?\s*)+)=\s*([\d,\s]+)$", jl, flags=re.M):
+        for n, v in zip([x.strip() for x in names.split(",") if x.strip()], vals.split(",")):
+            jlc[n[len("MODEL_"):]] = int(v)
+    for k, v in hdr.items():
+        assert getattr(_lib, "MODEL_" + k) == v, k
+        assert jlc[k] == v, k
+
+
 def test_struct_layouts_match_header():
     # sizes of the C structs (LP64): checked against a compiled probe of the header
     assert ct.sizeof(_lib.RunnerCfg) == 24

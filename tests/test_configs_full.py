@@ -3,7 +3,7 @@
 - config 5: Bayesian linear regression n=4096, d=512 (examples/linear_regression.jl:14-20; bench.py's
   `regression_data("linear", 4096, 512)`), `HMCDA()` with the reference defaults (HMCDA.jl:42-43: rate 0.65,
   len 2, shrinkage 0.05, t0 10, step 0.75).  d = 512 is the only regression width with no zero-padded columns of
-  the d-sliced kernel `glm_hmc<4, 8, true>` (8 waves of 64 coordinates per 16 chains), and n = 4096 runs 256 observation tiles
+  the d-sliced kernel `glm_hmc<8, 4, true>` (4 waves of 128 coordinates per 16 chains, two tiles a workgroup), and n = 4096 runs 256 observation tiles
   per evaluation.  With the NaN-initialised step (epsilon_0 = 1, HMCDA.jl:86-92) the first dual-averaging steps
   take trajectories of 2, 1, 2, 7 leapfrogs; by the fifth adapted step epsilon is ~0.07 and a step takes ~28
   leapfrogs of the default len = 2 -- so SerialMC(steps=7, burnin=5) runs the default trajectory length, not the
@@ -51,7 +51,7 @@ def test_config5_linear512_hmcda_defaults(gpu):
     r = mc.SerialMC(steps=7, burnin=5)
     t = (m * mc.HMCDA() * r).batch(C, seed=5)
     chain = mc.run(t)
-    assert t.step_kernel == "glm_hmc<4, 8, true>"
+    assert t.step_kernel == "glm_hmc<8, 4, true>"
     oc = orc.OracleChains(m, mc.HMCDA(), nchains=C, seed=5)
     s_ref, g_ref, acc_ref = oc.run(r, nthreads=ORC_THREADS)
     _check_chain(chain, oc, s_ref, g_ref, acc_ref)
