@@ -282,9 +282,13 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
     const int d = s.d;
     const int64_t cu = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (cu * CPW >= s.C) return;          // a tail wave with no live chain (no barriers below: it may leave)
-    // the wave's LDS slice for the layout changes: L NC doubles per chain
+    // the wave's LDS slice for the layout changes (L NC doubles per chain), and where x waits out the factor update
+    // (the update holds the column's entries, u, the next S z and its normals: x would take the registers that
+    // let three waves share a SIMD)
     __shared__ double xpose[kBlock / 64][64 * NC];
+    __shared__ double xpark[kBlock / 64][NC][64];
     double* const slice = &xpose[threadIdx.x >> 6][((threadIdx.x & 63) / L) * L * NC];
+    double (*const park)[64] = xpark[threadIdx.x >> 6];
     double x[NC];
     p.load(a.st.x, s.ld, x);
     double lp = p.load_scalar(a.st.lp);
@@ -349,7 +353,11 @@ __device__ __forceinline__ void ram_wave_body(const KernelArgs& a) {
                 a2 = __builtin_fma(zn[k], zn[k], a2);
             }
             ram_to_rows<NC, L>(slice, lane, zn, znr);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) park[k][threadIdx.x & 63] = x[k];
             ram_wave_update<NC, L, true>(Ss, Sd, vo, lane, d, alpha, nz, u, znr, un);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) x[k] = park[k][threadIdx.x & 63];
 #pragma unroll
             for (int k = 0; k < NC; ++k) u[k] = un[k];
             ram_to_quads<NC, L>(slice, lane, u, uq);
