@@ -455,6 +455,11 @@ __device__ __forceinline__ void glm_dma_tile(const double* img, double* buf) {
 }
 // GLM_DMA_SPREAD (default 0): the next tile's pieces issued between the eta MFMAs (one after every second MFMA)
 // instead of all before the eta operand reads
+// GLM_ETA_LA (default 8): how many eta A-operand reads run ahead of their MFMA in the 128-wide slices (NM = 8; the
+// 64-wide slices read all 16 before the first MFMA)
+#ifndef GLM_ETA_LA
+#define GLM_ETA_LA 8
+#endif
 #ifndef GLM_DMA_SPREAD
 #define GLM_DMA_SPREAD 0
 #endif
@@ -547,7 +552,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
         {
             constexpr int KM = 4 * NM;
-            constexpr int kLA = NM <= 4 ? KM : 8;
+            constexpr int kLA = NM <= 4 ? KM : GLM_ETA_LA;
             const double* xrow = LX + eta_lane;
             double av[KM];
 #pragma unroll
