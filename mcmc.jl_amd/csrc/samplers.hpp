@@ -230,6 +230,18 @@ struct PairChain {
         if (!defer) stage();
     }
     __device__ __forceinline__ void stage() const { bt.stage(); }
+    // the chain index as of this point: addresses formed from it after the step loop (state, lp) or on a kept step
+    // (accept bits) cannot be hoisted ahead of the loop and held -- at the 128-VGPR budget the held 64-bit addresses
+    // were spilled to scratch (3 x 8 B per lane, ~100 MB of scratch traffic per 2^20-chain launch)
+    __device__ __forceinline__ static uint32_t tid_now() {
+        uint32_t t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return t;
+    }
+    __device__ __forceinline__ int64_t c_now() const {
+        const uint32_t t = tid_now();
+        return (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)((t >> 6) * 32 + (t & 31));
+    }
     __device__ __forceinline__ int coord(int k) const { return h * NC + k; }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
     __device__ __forceinline__ uint32_t block(int b) const { return (uint32_t)(h * NB + b); }
@@ -268,7 +280,8 @@ struct PairChain {
     }
     __device__ __forceinline__ void store(double* x, int64_t ld, const double (&v)[NC]) const {
         if (!live) return;
-        uint64_t o = (uint64_t)c + (uint64_t)(h * NC) * (uint64_t)ld;
+        const int hn = (int)((tid_now() >> 5) & 1);
+        uint64_t o = (uint64_t)c_now() + (uint64_t)(hn * NC) * (uint64_t)ld;
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
             if (valid(k)) x[o] = v[k];
@@ -281,7 +294,7 @@ struct PairChain {
     __device__ __forceinline__ T load_t(const T* p) const { return p[live ? c : 0]; }
     template <class T>
     __device__ __forceinline__ void store_t(T* p, T v) const {
-        if (live && h == 0) p[c] = v;
+        if (live && h == 0) p[c_now()] = v;
     }
     __device__ __forceinline__ void store_kept(const StepArgs& s, int64_t kk, const double (&v)[NC],
                                                double* base) const {
@@ -312,9 +325,10 @@ struct PairChain {
     __device__ __forceinline__ void store_bit(const StepArgs& s, int64_t kk, bool acc) const {
         const uint64_t mask = __ballot(acc && live);
         if ((threadIdx.x & 63) == 0 && s.acc_bits != nullptr) {
-            const int64_t w = c >> 6;
+            const int64_t cc = c_now();
+            const int64_t w = cc >> 6;
             if (w < s.nw)
-                reinterpret_cast<uint32_t*>(s.acc_bits)[((size_t)kk * (size_t)s.nw + (size_t)w) * 2 + (size_t)((c >> 5) & 1)] =
+                reinterpret_cast<uint32_t*>(s.acc_bits)[((size_t)kk * (size_t)s.nw + (size_t)w) * 2 + (size_t)((cc >> 5) & 1)] =
                     (uint32_t)mask;
         }
     }
