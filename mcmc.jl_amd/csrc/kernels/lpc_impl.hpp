@@ -2,7 +2,6 @@
 // step code and its reference lines.  Included by one translation unit per model (lpc_<model>.hip)
 // so that the instantiations compile in parallel; lpc.hip dispatches on the model kind.
 #pragma once
-#include <cstdlib>
 #include "../samplers.hpp"
 #include "layout_api.hpp"
 
@@ -47,22 +46,6 @@ constexpr int lpp_mala_threads() { return F ? 768 : 512; }
 template <int NB, bool F, class M, bool US>
 __global__ __launch_bounds__(512, F && US ? 4 : 3) void lpp_rwm(KernelArgs a) {
     rwm_body<PairChain<NB, F, 512, kTabLds>, M, US>(a);
-}
-// the persistent RWM pair kernel (samplers.hpp rwm_persist_body): 2 blocks per CU, MCMCHIP_RWM_PERSIST=1 (A/B)
-template <int NB, bool F, class M, bool US>
-__global__ __launch_bounds__(512, F && US ? 4 : 3) void lpp_rwm_p(KernelArgs a, int32_t nblk) {
-    rwm_persist_body<PairChain<NB, F, 512, kTabLds>, M, US>(a, nblk);
-}
-static int rwm_persist_blocks() {
-    static const int v = [] {
-        const char* e = getenv("MCMCHIP_RWM_PERSIST");
-        if (e == nullptr || atoi(e) == 0) return 0;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 0;
-        return 2 * cus;
-    }();
-    return v;
 }
 template <int NB, bool F, class M>
 __global__ __launch_bounds__((lpp_mala_threads<NB, F>()), F ? 3 : 2) void lpp_mala(KernelArgs a) {
@@ -362,14 +345,6 @@ static hipError_t lpp_launch(const KernelArgs& a, hipStream_t st) {
     constexpr int TM = lpp_mala_threads<NBL, F>();
     switch (a.sa.kind) {
         case SK_RWM:
-            if constexpr (F) {
-                const int nblk = rwm_persist_blocks();
-                if (nblk > 0 && a.s.scale_uniform && (a.s.C + 255) / 256 > nblk) {
-                    mcmc_note_step_kernel("lpp_rwm_p<%d, %s, %s, %s>", NBL, b, M::kName, us);
-                    lpp_rwm_p<NBL, F, M, true><<<dim3((unsigned)nblk), 512, 0, st>>>(a, nblk);
-                    break;
-                }
-            }
             mcmc_note_step_kernel("lpp_rwm<%d, %s, %s, %s>", NBL, b, M::kName, us);
             if (a.s.scale_uniform) lpp_rwm<NBL, F, M, true><<<grid(512), 512, 0, st>>>(a);
             else lpp_rwm<NBL, F, M, false><<<grid(512), 512, 0, st>>>(a);

@@ -216,26 +216,18 @@ struct PairChain {
     static constexpr int kChainsPerBlock = TH / 2;
     static constexpr bool kPairs = true;
     int64_t c;        // local chain index
-    int64_t cbase;    // the block's first chain (wave-uniform)
     bool live;
     int d;
     int h;            // half: 0 (lanes 0-31) or 1 (lanes 32-63)
     BmTables<TAB, TH> bt;
     __device__ PairChain(const StepArgs& s, bool defer = false) {
         const int lane = (int)(threadIdx.x & 63);
-        cbase = (int64_t)blockIdx.x * kChainsPerBlock;
-        c = cbase + (int64_t)(threadIdx.x >> 6) * 32 + (lane & 31);
+        c = (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)(threadIdx.x >> 6) * 32 + (lane & 31);
         h = lane >> 5;
         live = c < s.C;
         d = s.d;
         bt.init();
         if (!defer) stage();
-    }
-    // a persistent block's next group of kChainsPerBlock chains (lpp_rwm_p)
-    __device__ __forceinline__ void rebase(const StepArgs& s, int64_t group) {
-        cbase = group * kChainsPerBlock;
-        c = cbase + (int64_t)(threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
-        live = c < s.C;
     }
     __device__ __forceinline__ void stage() const { bt.stage(); }
     // the chain index as of this point: addresses formed from it after the step loop (state, lp) or on a kept step
@@ -248,7 +240,7 @@ struct PairChain {
     }
     __device__ __forceinline__ int64_t c_now() const {
         const uint32_t t = tid_now();
-        return cbase + (int64_t)((t >> 6) * 32 + (t & 31));
+        return (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)((t >> 6) * 32 + (t & 31));
     }
     __device__ __forceinline__ int coord(int k) const { return h * NC + k; }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
@@ -646,75 +638,6 @@ __device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     p.store(a.st.x, s.ld, x);
     p.store_t(a.st.lp, lp);
     p.count_evals(s, s.nsteps);
-}
-
-// RWM over persistent blocks (lpp_rwm_p; P = PairChain): nblk blocks, two per CU, each staging the Box-Muller
-// tables once and visiting chain groups g = b, b + nblk, ... (kChainsPerBlock chains each) for the launch's steps.
-// A block in the second half of the grid (the second block of its CU when blocks are dealt to CUs round-robin)
-// splits its first group's steps into two visits, the second one last, so that the two blocks of a CU reach their
-// state loads and stores half a visit apart and one block's I/O runs beside the other's arithmetic.  Every visit is
-// rwm_body's loop over a contiguous step range (state through HBM between visits, as between launches), so the
-// chains are bitwise those of rwm_body.
-template <class P, class M, bool US>
-__device__ __forceinline__ void rwm_persist_body(const KernelArgs& a, int32_t nblk) {
-    const StepArgs& s = a.s;
-    P p(s, true);
-    p.stage();
-    const M model(a.m);
-    const Stream rs{s.key0, s.key1};
-    const int64_t ngroups = (s.C + P::kChainsPerBlock - 1) / P::kChainsPerBlock;
-    const int64_t b = blockIdx.x;
-    const bool late = b >= nblk / 2;
-    const int64_t half = s.nsteps / 2;
-    const int64_t ng = (ngroups - b + nblk - 1) / nblk;            // this block's groups
-    const bool split = late && half > 0;
-    const int64_t nv = ng + (split ? 1 : 0);
-    for (int64_t v = 0; v < nv; ++v) {
-        // visit v: (group, first step, end step); a split block visits its first group's first half first and its
-        // second half last
-        int64_t g = b + v * nblk, t0 = 0, t1 = s.nsteps;
-        if (split) {
-            if (v == 0) t1 = half;
-            else if (v == nv - 1) { g = b; t0 = half; }
-        }
-        g = __builtin_amdgcn_readfirstlane((int)g);
-        p.rebase(s, g);
-        const uint32_t chain = s.chain0 + (uint32_t)p.c;
-        double x[P::NC], sc[P::NC];
-        p.load(a.st.x, s.ld, x);
-        double lp = p.load_scalar(a.st.lp);
-#pragma unroll
-        for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
-        StepArgs sv = s;
-        sv.step_begin = s.step_begin + t0;
-        sv.nsteps = (int32_t)(t1 - t0);
-        AcceptDraw<P> ad;
-        Keeper keep(sv);
-        for (int t = 0; t < sv.nsteps; ++t) {
-            const int64_t i = sv.step_begin + t;
-            double xp[P::NC];
-            gen_normals(p, rs, chain, (uint32_t)i, xp);
-#pragma unroll
-            for (int k = 0; k < P::NC; ++k) xp[k] = x[k] + xp[k] * sc[k];
-            bool oos;
-            const double lpp = eval_lp(p, model, xp, oos);
-            const double ratio = lpp - lp;
-            const bool acc = ad.test(p, rs, chain, i, t, ratio);
-            if (acc) {
-#pragma unroll
-                for (int k = 0; k < P::NC; ++k) x[k] = xp[k];
-                lp = lpp;
-            }
-            int64_t kk;
-            if (keep.take(i, &kk)) {
-                p.store_kept(s, kk, x, s.samples);
-                p.store_bit(s, kk, acc);
-            }
-        }
-        p.store(a.st.x, s.ld, x);
-        p.store_t(a.st.lp, lp);
-        p.count_evals(s, sv.nsteps);
-    }
 }
 
 // ------------------------------------------------------------------ MALA
