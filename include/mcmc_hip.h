@@ -188,6 +188,16 @@ int mcmc_chains_create(mcmc_model* model, const mcmc_sampler_cfg* sampler, int64
 int mcmc_chains_destroy(mcmc_chains* chains);
 /* restart from model.init (resume(), SerialMC.jl:93-97): step counter back to 0. */
 int mcmc_chains_reset(mcmc_chains* chains);
+/* MCMC.reset(t, x) (src/MCMC.jl:39; the samplers' task-local :reset hooks, RWM.jl:49, MALA.jl:75-80, HMC.jl:114-116,
+ * HMCDA.jl:82-83, RAM.jl:47): every chain's position := x (host [d][nchains]) and its log-target (and gradient)
+ * re-evaluated there; lp (may be NULL) receives the log-targets [nchains].  The step counter, tuner state and RAM
+ * factor are kept.  Used by SeqMC-style drivers (SeqMC.jl:68-69) that move particles between tasks. */
+int mcmc_chains_set_state(mcmc_chains* chains, const double* x, double* lp);
+/* chains [first, first + count) of src as a new, independent batch (same model, sampler and seed; global chain ids
+ * src's + first) holding a copy of their whole state and step counter, so that running it continues exactly those
+ * chains whatever src does next.  No reference counterpart beyond run(c::MCMCChain) = run(c.task) (runners.jl:14):
+ * after one batched run of an Array{MCMCTask}, each returned chain's task continues its own chain. */
+int mcmc_chains_fork(mcmc_chains* src, int64_t first, int64_t count, mcmc_chains** out);
 /* steps consumed so far (the sampler's own loop counter i). */
 int mcmc_chains_steps_done(mcmc_chains* chains, int64_t* steps);
 /* per-chain adaptive state after the last run, [nchains] each (any may be NULL): step = the current step size

@@ -91,6 +91,7 @@ struct DevBuf {
 
 struct mcmc_chains {
     mcmc_model* model = nullptr;
+    mcmc_sampler_cfg cfg{};          // the sampler configuration it was created with (mcmc_chains_fork)
     SamplerArgs sa{};
     int64_t C = 0, ld = 0, offset = 0;
     uint64_t seed = 0;
@@ -704,6 +705,7 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     c->ld = ld_for(c->layout, nchains, d);
     c->offset = chain_offset;
     c->seed = seed;
+    c->cfg = *s;
     SamplerArgs& sa = c->sa;
     sa.kind = s->kind;
     sa.tuner = s->tuner;
@@ -810,6 +812,124 @@ extern "C" int mcmc_chains_reset(mcmc_chains* c) {
     if (!c) return fail(MCMC_E_INVALID_ARG, "chains is NULL");
     if (int r = set_device(c->model->ctx)) return r;
     return init_state(c);
+}
+
+// MCMC.reset(t, x) (MCMC.jl:39): the task-local :reset hook of every sampler (RWM.jl:49, MALA.jl:75-80,
+// HMC.jl:114-116, HMCDA.jl:82-83, RAM.jl:47) sets pars = x and re-evaluates the log-target (and gradient) there; the
+// step counter, the tuners' state and RAM's factor are left as they are.  x: host [d][C]; lp (may be NULL): host [C],
+// the log-targets at x.  A point out of support is accepted (the reference's hook does not assert): its log-target
+// is -Inf and the next proposal's ratio decides.
+extern "C" int mcmc_chains_set_state(mcmc_chains* c, const double* x, double* lp) {
+    if (!c || !x) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    mcmc_model* m = c->model;
+    mcmc_ctx* ctx = m->ctx;
+    if (int r = set_device(ctx)) return r;
+    const int d = m->args.d;
+    const int64_t C = c->C;
+    hipStream_t st = ctx->stream;
+    double* dcols = nullptr;
+    if (int r = dmalloc(&dcols, (size_t)d * C)) return r;
+    hipError_t e = hipMemcpyAsync(dcols, x, (size_t)d * C * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = cols_to_state(c->layout, c->st.x, c->ld, dcols, C, d, C, st);
+    KernelArgs a = base_args(m, C, c->ld);
+    if (e == hipSuccess) e = launch_eval(c->layout, a, c->st.x, c->st.lp, c->st.g, 0, st);
+    if (e == hipSuccess && lp) e = hipMemcpyAsync(lp, c->st.lp, (size_t)C * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamSynchronize(st);
+    dfree(dcols);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("set_state: ") + hipGetErrorString(e));
+    c->h_evals += C;                                    // model.eval(pars) once per chain
+    return MCMC_OK;
+}
+
+// chains [first, first + count) of src as an independent batch: the same model, sampler and seed, global chain ids
+// src's + first, and a copy of their whole state -- position, log-target, gradient, the tuners' per-chain state, RAM's
+// factor and the step counter -- so running the new batch continues exactly those chains (their random streams are
+// keyed by (seed, global chain, global step)), whatever src does afterwards.  Evaluation counts restart at 0.  Used
+// for run(t::Array{MCMCTask}) on GPU tasks: one batched launch, then every returned MCMCChain's task continues its own
+// chain (runners.jl:14).
+extern "C" int mcmc_chains_fork(mcmc_chains* src, int64_t first, int64_t count, mcmc_chains** out) {
+    if (!src || !out) return fail(MCMC_E_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (first < 0 || count <= 0 || first + count > src->C)
+        return fail(MCMC_E_INVALID_ARG, "fork: chains [" + std::to_string(first) + ", " + std::to_string(first + count) +
+                                            ") are not inside the batch of " + std::to_string(src->C));
+    mcmc_model* m = src->model;
+    mcmc_ctx* ctx = m->ctx;
+    if (int r = set_device(ctx)) return r;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipStreamSynchronize(st));
+    const int d = m->args.d;
+    std::vector<double> init;
+    if (src->d_init_x) {                                   // the forked chains' own starts (resume restarts there)
+        init.resize((size_t)d * count);
+        HIP_TRY(hipMemcpy2DAsync(init.data(), (size_t)count * 8, src->d_init_x + first, (size_t)src->C * 8,
+                                 (size_t)count * 8, (size_t)d, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    mcmc_chains* c = nullptr;
+    if (int r = mcmc_chains_create(m, &src->cfg, count, src->offset + first, src->seed,
+                                   init.empty() ? nullptr : init.data(), &c))
+        return r;
+    auto bail = [&](hipError_t e) {
+        mcmc_chains_destroy(c);
+        return fail(MCMC_E_HIP, std::string("fork: ") + hipGetErrorString(e));
+    };
+    auto cols = [&](double* dst, const double* from) -> hipError_t {       // per-coordinate rows or per-chain rows
+        if (!dst || !from) return hipSuccess;
+        if (c->layout == LAYOUT_WPC)
+            return hipMemcpyAsync(dst, from + (size_t)first * src->ld, (size_t)count * c->ld * 8,
+                                  hipMemcpyDeviceToDevice, st);
+        return hipMemcpy2DAsync(dst, (size_t)c->ld * 8, from + first, (size_t)src->ld * 8, (size_t)count * 8,
+                                (size_t)d, hipMemcpyDeviceToDevice, st);
+    };
+    auto vec = [&](void* dst, const void* from, size_t esz) -> hipError_t {
+        if (!dst || !from) return hipSuccess;
+        return hipMemcpyAsync(dst, (const char*)from + (size_t)first * esz, (size_t)count * esz,
+                              hipMemcpyDeviceToDevice, st);
+    };
+    hipError_t e = cols(c->st.x, src->st.x);
+    if (e == hipSuccess) e = cols(c->st.g, src->st.g);
+    if (e == hipSuccess) e = vec(c->st.lp, src->st.lp, 8);
+    if (e == hipSuccess) e = vec(c->st.t_step, src->st.t_step, 8);
+    if (e == hipSuccess) e = vec(c->st.t_bar, src->st.t_bar, 8);
+    if (e == hipSuccess) e = vec(c->st.t_h, src->st.t_h, 8);
+    if (e == hipSuccess) e = vec(c->st.t_leaps, src->st.t_leaps, 4);
+    if (e == hipSuccess) e = vec(c->st.t_acc, src->st.t_acc, 4);
+    if (e == hipSuccess) e = vec(c->st.t_prop, src->st.t_prop, 4);
+    if (e != hipSuccess) return bail(e);
+    if (src->st.ram_L) {
+        // the factor written last sits in half (steps_done & 1) of both batches (the step counter is copied)
+        const size_t half = (size_t)(src->steps_done & 1);
+        const double* sh = src->st.ram_L + half * (size_t)src->st.ram_hs;
+        double* dh = c->st.ram_L + half * (size_t)c->st.ram_hs;
+        if (c->layout == LAYOUT_WPC) {                     // [chain][ram_ld]
+            e = hipMemcpyAsync(dh, sh + (size_t)first * src->st.ram_ld, (size_t)count * c->st.ram_ld * 8,
+                               hipMemcpyDeviceToDevice, st);
+        } else {                                           // [64-chain tile][row][64]: re-tile on the host
+            const size_t tile = (ram_nrows(src->ram_dpad) + 1) * 64;
+            std::vector<double> hs(((size_t)src->C + 63) / 64 * tile), hd(((size_t)count + 63) / 64 * tile, 0.0);
+            e = hipMemcpyAsync(hs.data(), sh, hs.size() * 8, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(hd.data(), dh, hd.size() * 8, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e == hipSuccess) {
+                for (int64_t k = 0; k < count; ++k) {
+                    const size_t a = (size_t)(first + k), b = (size_t)k;
+                    for (size_t r = 0; r + 1 < tile / 64; ++r) hd[(b >> 6) * tile + r * 64 + (b & 63)] =
+                                                                   hs[(a >> 6) * tile + r * 64 + (a & 63)];
+                }
+                e = hipMemcpyAsync(dh, hd.data(), hd.size() * 8, hipMemcpyHostToDevice, st);
+            }
+        }
+        if (e != hipSuccess) return bail(e);
+    }
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return bail(e);
+    c->steps_done = src->steps_done;
+    c->spl = src->spl;
+    c->store_grads = src->store_grads;
+    *out = c;
+    return MCMC_OK;
 }
 
 extern "C" int mcmc_debug_chains_order(mcmc_chains* c, int32_t* used, int32_t* order) {

@@ -430,9 +430,10 @@ __device__ __forceinline__ double glm_eval1(const GlmArgs& a, const GlmPos& p, c
 // Written as inline asm: the compiler's waitcnt pass treats a __builtin_amdgcn_global_load_lds as an LDS store
 // that may alias every later ds_write, and put an s_waitcnt vmcnt(0) before the eta-partial store right after the
 // eta MFMAs -- draining the next tile's copy a few hundred cycles after it was issued (r04 ISA).  The asm is
-// opaque to that pass; M0 has no other user in the regression kernels (checked in the ISA: every s_mov_b32 m0 is
-// one of these).  Loads the pass does track stay correctly waited for: vmcnt decrements in issue order, so an
-// extra load in flight only makes its counted waits longer.
+// opaque to that pass.  The LDS address goes in through the "{m0}" operand constraint: the compiler writes M0
+// itself and knows what it holds afterwards (M0 is a reserved register, so a clobber would not be honoured).
+// Loads the pass does track stay correctly waited for: vmcnt decrements in issue order, so an extra load in flight
+// only makes its counted waits longer.
 template <int TS>
 constexpr int glm_dma_pieces_per_wave() { return (TS / 128 + 7) / 8; }
 // piece j (0 <= j < glm_dma_pieces_per_wave) of this wave's share of tile image img -> LDS buffer buf
@@ -445,7 +446,7 @@ __device__ __forceinline__ void glm_dma_piece(const double* img, double* buf, in
     if (c < kPieces) {
         const double* src = img + c * 128 + 2 * lane;
         const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(uintptr_t)buf + (uint32_t)c * 1024u));
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "s"(lds) : "memory");
+        asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src), "{m0}"(lds) : "memory");
     }
 }
 template <int TS>
@@ -1747,17 +1748,6 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
 #else
 hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st);
 
-// 128 < d <= 512: d-slices of 64 coordinates (NM = 4; the default, which the oracle restates) or, with
-// MCMCHIP_GLM_SLICE=128 (a dev A/B switch for benches only), of 128 (NM = 8, two 16-chain tiles per workgroup:
-// that build spills the HMC / MALA state at the 256-register budget, r04 measurements in DESIGN.md §5.3)
-static int glm_slice_override() {
-    static const int v = [] {
-        const char* e = getenv("MCMCHIP_GLM_SLICE");
-        return e != nullptr ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
     // d <= 128: one wave per 16-chain tile, DS = d_pad = 16 NM (NM a power of two, pipelined glm_eval1), 4 tiles
     // per workgroup;
@@ -1767,15 +1757,15 @@ mcmc::GlmShape mcmc_glm_shape(int d, int64_t n) {
     // 128-wide slices measured 0.30 against 0.53, two waves a tile);
     // 512 < d <= 1024: NW = 8 slices of DS = 128 coordinates (NM = 8), one tile per workgroup; d_pad = 1024 keeps
     // one LDS tile buffer (glm_xbufs).
-    // MCMCHIP_GLM_SLICE=64 / 128 forces the slice width for 128 < d <= 512 (bench A/B only: the oracle restates the
-    // default shapes).
+    // The slice geometry fixes each chain's summation order, so it is a function of d alone, restated by the oracle
+    // (orc_glm_geometry); no run-time switch changes it.
     mcmc::GlmShape g{};
     if (d <= 128) {
         int nm = 1;
         while (16 * nm < d) nm *= 2;
         g.nw = 1;
         g.nm = nm;
-    } else if (glm_slice_override() == 64 ? d <= 512 : (d <= 256 && glm_slice_override() != 128)) {
+    } else if (d <= 256) {
         int nw = 4;
         while (64 * nw < d) nw *= 2;
         g.nw = nw;

@@ -280,11 +280,16 @@ __global__ __launch_bounds__(kBlock) void lpc_rwm_spec(KernelArgs a) {
                     double xp[D];
 #pragma unroll
                     for (int k = 0; k < D; ++k) xp[k] = xs[k] + dz_l[buf][it][k];       // pars + randn(d) .* scale
-                    double acc0 = 0.0;
-#pragma unroll
-                    for (int k = 0; k < D; ++k) model.acc(acc0, xp[k]);
                     bool oos;
-                    const double lpp = llacc_finish(model, acc0, oos);                 // model.eval
+                    double lpp;                                                        // model.eval
+                    if constexpr (is_joint<M>::value) {
+                        lpp = model.joint_lp(xp, oos);              // a joint target (OU): no per-coordinate sum
+                    } else {
+                        double acc0 = 0.0;
+#pragma unroll
+                        for (int k = 0; k < D; ++k) model.acc(acc0, xp[k]);
+                        lpp = llacc_finish(model, acc0, oos);
+                    }
                     const double ratio = lpp - lps;
                     const bool acc = (ratio > 0.0) | (ratio > lu);                       // RWM.jl:63
                     const bool bi = (b >> i) & 1;

@@ -736,6 +736,8 @@ template <class P, class M>
 __device__ __forceinline__ double trajectory(const P& p, const M& model, double eps, int64_t nl, double (&x)[P::NC],
                                              double (&m)[P::NC]) {
     constexpr bool kCarry = P::NC <= 16;
+    // the uncarried branch reads model.grad per coordinate, which a joint model does not define (GradAt does)
+    static_assert(kCarry || !is_joint<M>::value, "joint models run lane per chain (NC <= 16)");
     bool oos = false;
     double lpl = 0.0;
     double kick[kCarry ? P::NC : 1];

@@ -57,6 +57,17 @@ function logistic_model(ctx, X::Matrix{Float64}, Y::Vector{Float64}; init = zero
     h[]
 end
 
+# examples/ornstein.jl:19-30: the series x (passed as Y), parameters (tau, sigma, mu) from the example's start and
+# scale hint (ornstein.jl:29-30)
+function ou_model(ctx, x::Vector{Float64}; init = [0.05, 1.0, 1.0], scale = [1000.0, 1.0, 10.0])
+    desc = ModelDesc(MODEL_OU, 1, 3, pointer(init), pointer(scale), 0.0, 1.0, 1.0, 1.0, 1.0, length(x), C_NULL,
+                     pointer(x), 0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve x init scale check(ccall((:mcmc_model_create, lib), Cint,
+        (Ptr{Cvoid}, Ref{ModelDesc}, Ptr{Ptr{Cvoid}}), ctx, desc, h))
+    h[]
+end
+
 rwm(scale) = SamplerCfg(RWM_K, scale, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 hmc(n, eps) = SamplerCfg(HMC_K, 0, 0, n, eps, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 hmcda(; rate=0.65, len=2., shrinkage=0.05, t0=10., step=0.75) =
@@ -68,6 +79,22 @@ function chains(model, s::SamplerCfg, nchains; seed = 1, offset = 0)
     check(ccall((:mcmc_chains_create, lib), Cint,
         (Ptr{Cvoid}, Ref{SamplerCfg}, Int64, Int64, UInt64, Ptr{Float64}, Ptr{Ptr{Cvoid}}),
         model, s, nchains, offset, seed, C_NULL, h))
+    h[]
+end
+
+# MCMC.reset(t, x) (MCMC.jl:39): every chain at x (d x C) with its log-target re-evaluated there; returns the lp
+function reset!(ch, x::Matrix{Float64})
+    lp = Vector{Float64}(undef, size(x, 2))
+    xt = collect(transpose(x))                                   # [d][C] in C order = Julia (C, d)
+    GC.@preserve xt lp check(ccall((:mcmc_chains_set_state, lib), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}),
+                                   ch, xt, lp))
+    lp
+end
+
+# chains first+1 .. first+count of ch as an independent batch that continues them (mcmc_chains_fork)
+function fork(ch, first::Integer, count::Integer)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:mcmc_chains_fork, lib), Cint, (Ptr{Cvoid}, Int64, Int64, Ptr{Ptr{Cvoid}}), ch, first, count, h))
     h[]
 end
 

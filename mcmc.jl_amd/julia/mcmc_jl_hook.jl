@@ -3,28 +3,34 @@
 # Target: the Julia the reference package is written for (Julia 0.3 syntax: `immutable`/`type`, `Union(...)`,
 # `{...}` Any-dicts, `Ptr{Void}`, `Uint8`, `finalizer(x, f)`, tasks with produce/consume).  It is include()d into
 # module MCMC, after src/runners/SerialMC.jl (INTEGRATION.md §Julia hook shows the one line), so it sees MCMCModel,
-# MCMCTask, MCMCChain, MCMCSample, SerialMC, RWM, MALA, HMC, HMCDA, RAM and EmpiricalMCMCTuner directly.  For
-# Julia >= 1.0 hosts without MCMC.jl, MCMCHip.jl is the plain binding of the same C ABI.
+# MCMCTask, MCMCChain, MCMCSample, HMCSample, SerialMC, RWM, MALA, HMC, HMCDA, RAM and EmpiricalMCMCTuner directly.
+# For Julia >= 1.0 hosts without MCMC.jl, MCMCHip.jl is the plain binding of the same C ABI.
 #
 # What it replaces, with no edit to the reference's own files:
-#   spinTask(m, s, r)         samplers.jl:53  -- a method for MCMCHipModel (more specific than MCMCModel): the task
-#                                                it returns produces MCMCSamples from GPU chains instead of
-#                                                SamplerTask's CPU loop, so `m * s * r` (MCMC.jl:87-98), run(t)
-#                                                and run_serialmc (runners.jl:7-11, SerialMC.jl:37-85), run(c) (the
-#                                                continuation, runners.jl:14) and resume (SerialMC.jl:93-97) all
-#                                                run unchanged on top of it;
-#   run(t::Array{MCMCTask})   runners.jl:17-33 -- hip_run_batch(m, s, r, nchains) instead: ONE batched launch of
-#                                                nchains independent chains (the reference's array of tasks, one
-#                                                chain each), returned as an Array{MCMCChain} built like
-#                                                run_serialmc's (DataFrame samples / gradients named from pmap,
-#                                                diagnostics {"step", "accept"}, runTime), or as raw arrays
-#                                                (hip_run_arrays) when a million DataFrames would not fit.
+#   spinTask(m, s, r)           samplers.jl:53  -- a method for MCMCHipModel (more specific than MCMCModel): the task
+#                                                  it returns produces MCMCSamples from a GPU chain instead of
+#                                                  SamplerTask's CPU loop, so `m * s * r` (MCMC.jl:87-98), run(t)
+#                                                  and run_serialmc (runners.jl:7-11, SerialMC.jl:37-85), run(c) (the
+#                                                  continuation, runners.jl:14) and resume (SerialMC.jl:93-97) all
+#                                                  run unchanged on top of it.  Each task installs the :reset hook
+#                                                  (RWM.jl:49 ...) that MCMC.reset (MCMC.jl:39) and SeqMC
+#                                                  (SeqMC.jl:68-69) call;
+#   run(t::Array{MCMCTask})     runners.jl:17-33 -- redefined: tasks spun from one GPU model, sampler and runner (and
+#                                                  not yet started) run as ONE chain batch, one mcmc_run_serialmc;
+#                                                  each returned MCMCChain's task continues its own chain.  Any
+#                                                  other array goes through the reference's dispatch as before;
+#   prun(t::Array{MCMCTask})    runners.jl:35-42 -- redefined likewise: like GPU tasks as one batch, then stopped
+#                                                  (run_serialmc_exit); other arrays pmap as before.
+# Random streams.  The reference's tasks draw from Julia's global RNG as they run, so every spun task samples a
+# chain of its own.  A GPU chain's stream is (Philox key, global chain id), so the mirror of the global RNG is
+# hip_stream: a key plus a cursor over chain ids (hip_srand(seed) restarts it); a task takes its id when it first
+# runs.
 # Text only in this repository: the image has no Julia.  Struct layouts mirror include/mcmc_hip.h field for field
 # (tests/test_api_cpu.py::test_julia_hook_structs_mirror_header checks the field lists against the header).
 
 const hiplib = haskey(ENV, "MCMCHIP_LIB") ? ENV["MCMCHIP_LIB"] : "libmcmc_hip"
 
-export MCMCHipModel, hipmodel, hip_run_batch, hip_run_arrays
+export MCMCHipModel, hipmodel, hip_run_batch, hip_run_arrays, hip_srand
 
 # ---- C structs (include/mcmc_hip.h), isbits, C layout
 immutable HipModelDesc            # mcmc_model_desc
@@ -50,7 +56,7 @@ type HipOutputs                   # mcmc_outputs (the library writes runtime_s, 
 end
 
 const HIP_MODEL_KINDS = {:isonormal_dot => 1, :normal => 2, :logistic => 3, :linear => 4, :absnormal => 5, :dist => 6,
-                         :probit => 7, :dist_obs => 8}
+                         :probit => 7, :dist_obs => 8, :ou => 9}
 const HIP_DISTS = {:Normal => 1, :Uniform => 2, :Weibull => 3, :Beta => 4, :TDist => 5, :Exponential => 6,
                    :Gamma => 7, :Cauchy => 8, :LogNormal => 9, :Laplace => 10}
 
@@ -81,21 +87,32 @@ end
 # hipmodel(:probit; X=X, Y=y, prior_sigma=10.)                  examples/probit_regression.jl:18-40
 # hipmodel(:dist_obs; dist=:Normal, mu=1., sigma=1., Y=ones(1000), init=[1.])
 #                                                               model(:(y = x * v; y ~ Normal(1, 1)), x=1.)
+# hipmodel(:ou; Y=x, init=[0.05, 1., 1.], scale=[1000., 1., 10.])
+#                                                               examples/ornstein.jl:19-30 (the series x in Y; the
+#                                                               chain's columns tau, sigma, mu as model(ex, tau=...) names)
 function hipmodel(kind::Symbol; init::Vector{Float64}=Float64[], scale::Vector{Float64}=Float64[],
                   name::Symbol=:vars, gradient::Bool=true, mu::Float64=0., sigma::Float64=1., dist::Symbol=:Normal,
                   prior_sigma::Float64=1., noise_sigma::Float64=1., link_sign::Float64=1.,
-                  X::Matrix{Float64}=zeros(0, 0), Y::Vector{Float64}=Float64[], device::Int=0)
+                  X::Matrix{Float64}=zeros(0, 0), Y::Vector{Float64}=Float64[], device::Int=0,
+                  pmap::Union(Dict, Nothing)=nothing)
   @assert haskey(HIP_MODEL_KINDS, kind) "unknown GPU model kind $kind"
   if kind == :logistic || kind == :linear || kind == :probit
     @assert size(X, 1) == length(Y) "X has $(size(X, 1)) rows, Y $(length(Y)) entries"
     isempty(init) && (init = zeros(size(X, 2)))
   end
   kind == :dist_obs && (@assert length(init) == 1 "y = x * v: x is a scalar"; @assert !isempty(Y) "the data v in Y")
+  if kind == :ou
+    @assert length(init) == 3 "the Ornstein-Uhlenbeck model has 3 parameters (tau, sigma, mu)"
+    @assert length(Y) >= 2 "the Ornstein-Uhlenbeck model needs a series of at least 2 values in Y"
+    pmap == nothing && (pmap = {:tau => (1, ()), :sigma => (2, ()), :mu => (3, ())})
+  end
   d = length(init)
   @assert d > 0 "init must hold the parameter vector"
   isempty(scale) && (scale = ones(d))
   @assert length(scale) == d "scale parameter size ($(length(scale))) different from initial values ($d)"
-  pmap = d == 1 ? {name => (1, ())} : {name => (1, (d,))}       # one scalar or vector variable, as model() builds
+  if pmap == nothing
+    pmap = d == 1 ? {name => (1, ())} : {name => (1, (d,))}     # one scalar or vector variable, as model() builds
+  end
   MCMCHipModel(kind, d, copy(init), copy(scale), pmap, gradient, mu, sigma, dist, prior_sigma, noise_sigma,
                link_sign, X, Y, device)
 end
@@ -111,18 +128,22 @@ end
 # ---- samplers (RWM.jl:24-36, MALA.jl:50-62, HMC.jl:53-74, HMCDA.jl:24-43, RAM.jl:22-35)
 hip_tuner(t) = t == nothing ? (0, 0, 0, 0., 0.) :
   (1, t.adaptStep, t.maxStep, t.targetPath, t.targetRate)      # EmpiricalMCMCTuner (samplers.jl:32-50)
-hip_cfg(kind, scale, drift, nl, ls, rate, len, shr, t0, st, tu) =
-  HipSamplerCfg(kind, scale, drift, nl, ls, rate, len, shr, t0, st, tu[1], tu[2], tu[3], tu[4], tu[5], 0)
+hip_cfg(kind, scale, drift, nl, ls, rate, len, shr, t0, st, tu, maxl) =
+  HipSamplerCfg(kind, scale, drift, nl, ls, rate, len, shr, t0, st, tu[1], tu[2], tu[3], tu[4], tu[5], maxl)
 hip_sampler(s::RWM) = (s.tuner == nothing || error("RWM tuners are not built for the GPU");
-                       hip_cfg(1, s.scale, 0., 0, 0., 0., 0., 0., 0., 0., hip_tuner(nothing)))
-hip_sampler(s::MALA) = hip_cfg(2, 0., s.driftStep, 0, 0., 0., 0., 0., 0., 0., hip_tuner(s.tuner))
-# storeLeaps (HMC.jl:145-150): the C ABI records trajectories (mcmc_chains_store_leaps); this hook does not map them
-# into diagnostics["leaps"] yet, so it refuses rather than drop them
-hip_sampler(s::HMC) = (s.storeLeaps && error("storeLeaps: use MCMCHip.jl / mcmc_chains_store_leaps");
-                       hip_cfg(3, 0., 0., s.nLeaps, s.leapStep, 0., 0., 0., 0., 0., hip_tuner(s.tuner)))
-hip_sampler(s::HMCDA) = (s.storeLeaps && error("storeLeaps: use MCMCHip.jl / mcmc_chains_store_leaps");
-                         hip_cfg(4, 0., 0., 0, 0., s.rate, s.len, s.shrinkage, s.t0, s.step, hip_tuner(nothing)))
-hip_sampler(s::RAM) = hip_cfg(5, s.scale, 0., 0, 0., s.rate, 0., 0., 0., 0., hip_tuner(nothing))
+                       hip_cfg(1, s.scale, 0., 0, 0., 0., 0., 0., 0., 0., hip_tuner(nothing), 0))
+hip_sampler(s::MALA) = hip_cfg(2, 0., s.driftStep, 0, 0., 0., 0., 0., 0., 0., hip_tuner(s.tuner), 0)
+hip_sampler(s::HMC) = hip_cfg(3, 0., 0., s.nLeaps, s.leapStep, 0., 0., 0., 0., 0., hip_tuner(s.tuner), 0)
+hip_sampler(s::HMCDA) = hip_cfg(4, 0., 0., 0, 0., s.rate, s.len, s.shrinkage, s.t0, s.step, hip_tuner(nothing), 0)
+hip_sampler(s::RAM) = hip_cfg(5, s.scale, 0., 0, 0., s.rate, 0., 0., 0., 0., hip_tuner(nothing), 0)
+
+# storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117): leapfrog states recorded per step, up to a cap -- the trajectory
+# length for HMC (the tuner's maxStep bound when tuned), hip_leap_cap for HMCDA, whose length round(len / leapStep)
+# adapts (a longer trajectory is an error rather than a truncated record)
+const hip_leap_cap = 1024
+hip_store_leaps(s::MCMCSampler) = (isa(s, HMC) || isa(s, HMCDA)) && s.storeLeaps
+hip_leaps_cap(s::HMC) = s.tuner == nothing ? s.nLeaps : max(s.nLeaps, s.tuner.maxStep)
+hip_leaps_cap(s::HMCDA) = hip_leap_cap
 
 # ---- device objects, released by finalizers (chains before their model, the model before its context: each
 #      holds a reference to its parent, so the parent is still reachable while the child is alive)
@@ -159,60 +180,196 @@ type HipChains
     hipcheck(ccall((:mcmc_chains_create, hiplib), Cint,
                    (Ptr{Void}, Ptr{HipSamplerCfg}, Int64, Int64, Uint64, Ptr{Float64}, Ptr{Ptr{Void}}),
                    mh.h, [cfg], nchains, offset, seed, convert(Ptr{Float64}, C_NULL), h))   # every chain at init
-    c = new(h[1], mh, d, nchains)
-    finalizer(c, x -> (x.h == C_NULL || ccall((:mcmc_chains_destroy, hiplib), Cint, (Ptr{Void},), x.h); x.h = C_NULL))
-    c
+    hip_chains_owned(new(h[1], mh, d, nchains))
   end
+  # chains [first, first + count) of src (0-based first), state and step counter copied: mcmc_chains_fork
+  function HipChains(src::HipChains, first::Int, count::Int)
+    h = Array(Ptr{Void}, 1)
+    hipcheck(ccall((:mcmc_chains_fork, hiplib), Cint, (Ptr{Void}, Int64, Int64, Ptr{Ptr{Void}}),
+                   src.h, first, count, h))
+    hip_chains_owned(new(h[1], src.model, src.d, count))
+  end
+end
+hip_chains_owned(c::HipChains) =
+  (finalizer(c, x -> (x.h == C_NULL || ccall((:mcmc_chains_destroy, hiplib), Cint, (Ptr{Void},), x.h); x.h = C_NULL));
+   c)
+
+# MCMC.reset's device side: every chain of ch at x (d x nchains), log-targets returned (mcmc_chains_set_state)
+function hip_set_state!(ch::HipChains, x::Matrix{Float64})
+  lp = Array(Float64, ch.nchains)
+  hipcheck(ccall((:mcmc_chains_set_state, hiplib), Cint, (Ptr{Void}, Ptr{Float64}, Ptr{Float64}),
+                 ch.h, x', lp))                  # [d][C] in C order = Julia (C, d)
+  lp
 end
 
 const hip_contexts = Dict{Int, HipContext}()
 hip_context(dev::Int) = haskey(hip_contexts, dev) ? hip_contexts[dev] : (hip_contexts[dev] = HipContext(dev))
 
-hip_chains(m::MCMCHipModel, s::MCMCSampler, nchains::Int, seed::Int) =
-  HipChains(HipModelHandle(hip_context(m.device), m), hip_sampler(s), m.size, nchains, seed, 0)
+hip_chains(m::MCMCHipModel, s::MCMCSampler, nchains::Int, seed::Int, offset::Int) =
+  HipChains(HipModelHandle(hip_context(m.device), m), hip_sampler(s), m.size, nchains, seed, offset)
+
+# ---- the global stream (see the header): hip_draw(n) takes n consecutive global chain ids; ids are 32-bit (the
+#      Philox counter's chain word), so a cursor that would pass 2^32 moves on to the next key
+type HipStream
+  seed::Int
+  next::Int
+end
+const hip_stream = HipStream(1, 0)
+hip_srand(seed::Int) = (hip_stream.seed = seed; hip_stream.next = 0; nothing)
+function hip_draw(n::Int)
+  if hip_stream.next + n > 2^32
+    hip_stream.seed += 1
+    hip_stream.next = 0
+  end
+  first = hip_stream.next
+  hip_stream.next += n
+  (hip_stream.seed, first)
+end
 
 # one mcmc_run_serialmc of `len` steps, rows (burnin+1):thinning:len kept: samples / gradients [nkept*d*C]
-# ([nkept][d][C] in C order = Julia (C, d, nkept) column-major), accept bits [nkept][ceil(C/64)]
-function hip_run!(ch::HipChains, burnin::Int, thinning::Int, len::Int, grads::Bool)
+# ([nkept][d][C] in C order = Julia (C, d, nkept) column-major), accept bits [nkept][ceil(C/64)], the final state
+# (C, d) and log-targets; with cap >= 0 the storeLeaps record of every kept step (mcmc_chains_store_leaps):
+# pars / grad / m as Julia (C, d, cap+1, nkept), logTarget / H (C, cap+1, nkept), nleaps (C, nkept)
+type HipRun
+  x::Array{Float64, 3}
+  g::Array{Float64, 3}
+  bits::Matrix{Uint64}
+  fx::Matrix{Float64}
+  flp::Vector{Float64}
+  runtime::Float64
+  leaps::Dict
+end
+hip_accept(o::HipRun, j::Int, c::Int) = (o.bits[div(c - 1, 64) + 1, j] >> ((c - 1) % 64)) & 1 == 1
+
+function hip_run!(ch::HipChains, burnin::Int, thinning::Int, len::Int, grads::Bool, cap::Int=-1)
   nk = length((burnin + 1):thinning:len)
   C, d, nw = ch.nchains, ch.d, div(ch.nchains + 63, 64)
   x = Array(Float64, C, d, nk)
   g = grads ? Array(Float64, C, d, nk) : Array(Float64, 0, 0, 0)
   bits = Array(Uint64, nw, nk)
+  fx = Array(Float64, C, d)
+  flp = Array(Float64, C)
+  leaps = Dict()
+  if cap >= 0
+    for k in (:pars, :grad, :m); leaps[k] = Array(Float64, C, d, cap + 1, nk); end
+    for k in (:logTarget, :H); leaps[k] = Array(Float64, C, cap + 1, nk); end
+    leaps[:nleaps] = Array(Int32, C, nk)
+    hipcheck(ccall((:mcmc_chains_store_leaps, hiplib), Cint,
+                   (Ptr{Void}, Int64, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                   ch.h, cap, leaps[:pars], leaps[:grad], leaps[:m], leaps[:logTarget], leaps[:H], leaps[:nleaps]))
+  end
   out = HipOutputs(pointer(x), grads ? pointer(g) : convert(Ptr{Float64}, C_NULL), pointer(bits),
-                   convert(Ptr{Float64}, C_NULL), convert(Ptr{Float64}, C_NULL), 0, 0., 0., 0)
+                   pointer(fx), pointer(flp), 0, 0., 0., 0)
   hipcheck(ccall((:mcmc_run_serialmc, hiplib), Cint, (Ptr{Void}, Ptr{HipRunnerCfg}, Ptr{HipOutputs}),
                  ch.h, [HipRunnerCfg(burnin, thinning, len)], &out))
-  accept(j, c) = (bits[div(c - 1, 64) + 1, j] >> ((c - 1) % 64)) & 1 == 1
-  x, g, accept, out.runtime_s
+  HipRun(x, g, bits, fx, flp, out.runtime_s, leaps)
 end
 
 has_grads(s::MCMCSampler) = isa(s, MALA) || isa(s, HMC) || isa(s, HMCDA)
 
-# ---- drop-in: spinTask for GPU models.  The Julia Task produces one MCMCSample per step, as SamplerTask does,
-#      from GPU runs of `chunk` steps (every step kept); run_serialmc consumes them and builds the MCMCChain
-#      itself.  plogtarget / pars / logtarget carry NaN: run_serialmc reads only ppars, pgrads and diagnostics.
+# diagnostics["leaps"] of kept step j, chain c: the reference's leapStates, HMCSample(pars, grad, m, logTarget, H)
+# for leap 0 (state0 after update!) .. nLeaps
+function hip_leap_states(o::HipRun, j::Int, c::Int, cap::Int)
+  nl = int(o.leaps[:nleaps][c, j])
+  nl > cap && error("storeLeaps: a trajectory of $nl leapfrogs exceeds the recording cap $cap")
+  L = o.leaps
+  HMCSample[HMCSample(vec(L[:pars][c, :, l, j]), vec(L[:grad][c, :, l, j]), vec(L[:m][c, :, l, j]),
+                      L[:logTarget][c, l, j], L[:H][c, l, j]) for l in 1:(nl + 1)]
+end
+
+# ---- per-task state, shared by a GPU task's producer loop and the batched runners (hip_tasks maps the Julia Task
+#      of an MCMCTask to it)
+type HipTaskState
+  model::MCMCHipModel
+  sampler::MCMCSampler
+  chains::Union(HipChains, Nothing)   # the task's one GPU chain, made on first use
+  src::Union(HipChains, Nothing)      # after a batched run: the batch, whose chain `first` this task continues
+  first::Int
+  seed::Int
+  offset::Int                         # global chain id; -1 until drawn
+  stopped::Bool
+  buf::Union(HipRun, Nothing)         # chunk mode: steps run ahead on the GPU, produced one by one
+  pos::Int
+  single::Bool                        # after a reset: one GPU step per consume, with the log-targets it produced
+  x::Vector{Float64}
+  lp::Float64
+end
+HipTaskState(m::MCMCHipModel, s::MCMCSampler) =
+  HipTaskState(m, s, nothing, nothing, 0, 0, -1, false, nothing, 0, false, Float64[], NaN)
+const hip_tasks = WeakKeyDict()
+
+function hip_ensure!(st::HipTaskState)
+  st.stopped && error("the task was stopped by prun (run_serialmc_exit, SerialMC.jl:87-91)")
+  st.chains != nothing && return st.chains
+  if st.src != nothing                                   # continue chain `first` of a batched run
+    st.chains = HipChains(st.src, st.first, 1)
+    st.src = nothing
+  else
+    st.seed, st.offset = hip_draw(1)
+    st.chains = hip_chains(st.model, st.sampler, 1, st.seed, st.offset)
+  end
+  st.chains
+end
+
+# the :reset hook: the chain jumps to x, its log-target re-evaluated there (the samplers' hooks, RWM.jl:49,
+# MALA.jl:75-80, HMC.jl:114-116, HMCDA.jl:82-83, RAM.jl:47); buffered steps are dropped and the task turns to one
+# GPU step per consume, so that every MCMCSample carries plogtarget and logtarget (SeqMC.jl:69-72 reads them)
+function hip_reset!(st::HipTaskState, x::Vector{Float64})
+  ch = hip_ensure!(st)
+  st.lp = hip_set_state!(ch, reshape(copy(x), length(x), 1))[1]
+  st.x = copy(x)
+  st.buf = nothing
+  st.single = true
+  nothing
+end
+
+# ---- drop-in: spinTask for GPU models.  The Julia Task produces one MCMCSample per step, as SamplerTask does:
+#      from GPU runs of `chunk` steps (every step kept; plogtarget / pars / logtarget NaN: run_serialmc reads only
+#      ppars, pgrads and diagnostics), or, after MCMC.reset, from single GPU steps with their log-targets.
 #      A continuation (run(c), runners.jl:14) keeps consuming the same task, i.e. the same GPU chain.
 const hip_chunk = 1000
-function spinTask(m::MCMCHipModel, s::MCMCSampler, r::MCMCRunner)
-  seed = 1
-  task = Task(() -> begin
-    ch = hip_chains(m, s, 1, seed)
-    grads = has_grads(s)
-    nan = fill(NaN, m.size)
-    while true
-      x, g, accept, _ = hip_run!(ch, 0, 1, hip_chunk, grads)
-      for j in 1:hip_chunk
-        diag = Dict{Any, Any}()
-        diag["accept"] = accept(j, 1)
-        produce(MCMCSample(vec(x[1, :, j]), NaN, grads ? vec(g[1, :, j]) : nothing, nan, NaN, nothing, diag))
+hip_chunk_len(st::HipTaskState, cap::Int) =
+  cap < 0 ? hip_chunk : max(1, min(hip_chunk, div(1 << 28, 8 * (cap + 1) * (3 * st.model.size + 2))))
+
+function hip_produce_loop(st::HipTaskState)
+  task_local_storage(:reset, (resetPars::Vector{Float64}) -> hip_reset!(st, resetPars))
+  grads = has_grads(st.sampler)
+  cap = hip_store_leaps(st.sampler) ? hip_leaps_cap(st.sampler) : -1
+  nan = fill(NaN, st.model.size)
+  while true
+    ch = hip_ensure!(st)
+    if st.single
+      o = hip_run!(ch, 0, 1, 1, grads, cap)
+      diag = Dict{Any, Any}()
+      diag["accept"] = hip_accept(o, 1, 1)
+      cap >= 0 && (diag["leaps"] = hip_leap_states(o, 1, 1, cap))
+      x1, lp1 = vec(o.fx[1, :]), o.flp[1]
+      produce(MCMCSample(x1, lp1, grads ? vec(o.g[1, :, 1]) : nothing, st.x, st.lp, nothing, diag))
+      st.x, st.lp = x1, lp1
+    else
+      if st.buf == nothing || st.pos > size(st.buf.x, 3)
+        st.buf = hip_run!(ch, 0, 1, hip_chunk_len(st, cap), grads, cap)
+        st.pos = 1
       end
+      o, j = st.buf, st.pos
+      st.pos += 1
+      diag = Dict{Any, Any}()
+      diag["accept"] = hip_accept(o, j, 1)
+      cap >= 0 && (diag["leaps"] = hip_leap_states(o, j, 1, cap))
+      produce(MCMCSample(vec(o.x[1, :, j]), NaN, grads ? vec(o.g[1, :, j]) : nothing, nan, NaN, nothing, diag))
     end
-  end)
+  end
+end
+
+function spinTask(m::MCMCHipModel, s::MCMCSampler, r::MCMCRunner)
+  hip_sampler(s)                                         # refuse unsupported configurations now, as the ctor would
+  st = HipTaskState(m, s)
+  task = Task(() -> hip_produce_loop(st))
+  hip_tasks[task] = st
   MCMCTask(task, m, s, r)
 end
 
-# ---- batched: nchains independent chains in one launch (the reference: an Array{MCMCTask}, one chain each)
+# ---- batched: like tasks as one chain batch
 function hip_colnames(m::MCMCHipModel)
   cn = Array(ASCIIString, m.size)
   for (k, v) in m.pmap
@@ -227,29 +384,96 @@ function hip_colnames(m::MCMCHipModel)
   cn
 end
 
-# raw arrays: samples / gradients (C, d, nkept), accept (nkept, C) Bool, runTime -- for batches whose per-chain
-# DataFrames would not fit in host memory
-function hip_run_arrays(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, nchains::Int; seed::Int=1)
-  ch = hip_chains(m, s, nchains, seed)
-  x, g, accept, rt = hip_run!(ch, r.burnin, r.thinning, r.len, has_grads(s))
-  nk = size(x, 3)
-  acc = Bool[accept(j, c) for j in 1:nk, c in 1:nchains]
-  x, g, acc, rt
+# chain c of a batched run, built like run_serialmc's (SerialMC.jl:37-85): samples / gradients DataFrames with the
+# pmap column names, diagnostics {"step" => collect(r), "accept" => Bool[] (, "leaps")}, the batch's runTime
+function hip_chain(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, o::HipRun, c::Int, t::MCMCTask)
+  cn = hip_colnames(m)
+  nk = size(o.x, 3)
+  sc = reshape(o.x[c, :, :], m.size, nk)'                               # nkept x d
+  gd = has_grads(s) ? DataFrame(reshape(o.g[c, :, :], m.size, nk)', cn) : DataFrame()
+  diags = {"step" => collect(r.r), "accept" => Bool[hip_accept(o, j, c) for j in 1:nk]}
+  if hip_store_leaps(s)
+    cap = hip_leaps_cap(s)
+    diags["leaps"] = Array{HMCSample}[hip_leap_states(o, j, c, cap) for j in 1:nk]
+  end
+  MCMCChain(r.r, DataFrame(sc, cn), gd, diags, t, o.runtime)
 end
 
-# an Array{MCMCChain}, chain c built like run_serialmc's (SerialMC.jl:37-85): samples / gradients DataFrames with
-# the pmap column names, diagnostics {"step" => collect(r), "accept" => Bool[]}, the batch's runTime; each chain's
-# task field is a spinTask of its own (a continuation of it restarts a single GPU chain from model.init)
-function hip_run_batch(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, nchains::Int; seed::Int=1)
-  x, g, acc, rt = hip_run_arrays(m, s, r, nchains; seed=seed)
-  cn = hip_colnames(m)
-  grads = has_grads(s)
-  res = Array(MCMCChain, nchains)
-  for c in 1:nchains
-    sc = x[c, :, :]; sc = reshape(sc, size(sc, 2), size(sc, 3))'          # nkept x d
-    diags = {"step" => collect(r.r), "accept" => acc[:, c]}
-    gd = grads ? (gc = reshape(g[c, :, :], m.size, size(g, 3))'; DataFrame(gc, cn)) : DataFrame()
-    res[c] = MCMCChain(r.r, DataFrame(sc, cn), gd, diags, spinTask(m, s, r), rt)
+# tasks that can share one batch: GPU tasks of one model object, one sampler configuration and one SerialMC runner,
+# none started yet
+function hip_batchable(t::Array{MCMCTask})
+  isempty(t) && return false
+  t1 = t[1]
+  isa(t1.model, MCMCHipModel) && isa(t1.runner, SerialMC) || return false
+  cfg1 = hip_sampler(t1.sampler)
+  for x in t
+    haskey(hip_tasks, x.task) || return false
+    st = hip_tasks[x.task]
+    (st.chains == nothing && st.src == nothing && !st.stopped) || return false
+    (x.model === t1.model && isa(x.runner, SerialMC)) || return false
+    (x.runner.burnin, x.runner.thinning, x.runner.len) == (t1.runner.burnin, t1.runner.thinning, t1.runner.len) ||
+      return false
+    (hip_sampler(x.sampler) == cfg1 && hip_store_leaps(x.sampler) == hip_store_leaps(t1.sampler)) || return false
+  end
+  true
+end
+
+# one mcmc_run_serialmc for every task of t (consecutive global chain ids from the stream); task k then continues
+# chain k (a fork of the batch's state on its first use) or, with stop (prun), is stopped (run_serialmc_exit)
+function hip_run_tasks(t::Array{MCMCTask}, stop::Bool)
+  m, s, r = t[1].model, t[1].sampler, t[1].runner
+  n = length(t)
+  seed, first = hip_draw(n)
+  ch = hip_chains(m, s, n, seed, first)
+  cap = hip_store_leaps(s) ? hip_leaps_cap(s) : -1
+  o = hip_run!(ch, r.burnin, r.thinning, r.len, has_grads(s), cap)
+  res = Array(MCMCChain, size(t))
+  for k in 1:n
+    st = hip_tasks[t[k].task]
+    st.seed, st.offset = seed, first + k - 1
+    if stop
+      st.stopped = true
+    else
+      st.src, st.first = ch, k - 1
+    end
+    res[k] = hip_chain(m, s, r, o, k, t[k])
+    stop && stop!(res[k])
   end
   res
+end
+
+# run(t::Array{MCMCTask}) (runners.jl:17-33): like GPU tasks as one batch; every other array as the reference runs it
+function run(t::Array{MCMCTask}; args...)
+  lastrunner = t[end].runner
+  @assert all(map(x -> isa(x.runner, typeof(lastrunner)), t)) "Runners do not have the same runner type"
+  isa(lastrunner, SerialMC) && hip_batchable(t) && return hip_run_tasks(t, false)
+  if isa(lastrunner, SerialMC)
+    res = Array(MCMCChain, size(t))
+    for i in 1:length(t); res[i] = run(t[i]); end
+    return res
+  end
+  isa(lastrunner, SerialTempMC) && return run_serialtempmc(t)
+  run_seqmc(t; args...)
+end
+
+# prun(t::Array{MCMCTask}) (runners.jl:35-42): like GPU tasks as one batch, then stopped; others pmap as before
+function prun(t::Array{MCMCTask}; args...)
+  lastrunner = t[end].runner
+  @assert all(map(x -> isa(x.runner, typeof(lastrunner)), t)) "Runners do not have the same runner type"
+  isa(lastrunner, SerialMC) || return nothing
+  hip_batchable(t) && return hip_run_tasks(t, true)
+  pmap(run_serialmc_exit, t)
+end
+
+# nchains independent chains as one batch, each returned MCMCChain's task continuing its own chain
+hip_run_batch(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, nchains::Int) =
+  run(MCMCTask[spinTask(m, s, r) for i in 1:nchains])
+
+# raw arrays: samples / gradients (C, d, nkept), accept (nkept, C) Bool, runTime -- for batches whose per-chain
+# DataFrames would not fit in host memory; the chains come from the global stream
+function hip_run_arrays(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, nchains::Int)
+  seed, first = hip_draw(nchains)
+  o = hip_run!(hip_chains(m, s, nchains, seed, first), r.burnin, r.thinning, r.len, has_grads(s))
+  nk = size(o.x, 3)
+  o.x, o.g, Bool[hip_accept(o, j, c) for j in 1:nk, c in 1:nchains], o.runtime
 end

@@ -50,7 +50,8 @@ EXPORTED_SYMBOLS = (
     "mcmc_ctx_create", "mcmc_ctx_destroy", "mcmc_ctx_synchronize",
     "mcmc_model_create", "mcmc_model_destroy", "mcmc_model_eval",
     "mcmc_sampler_validate", "mcmc_runner_validate",
-    "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_steps_done", "mcmc_chains_evals",
+    "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_set_state", "mcmc_chains_fork",
+    "mcmc_chains_steps_done", "mcmc_chains_evals",
     "mcmc_chains_ram_factor", "mcmc_chains_tuner_state",
     "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients", "mcmc_chains_reserve_outputs",
     "mcmc_chains_launches", "mcmc_chains_step_kernel", "mcmc_chains_store_leaps", "mcmc_run_serialmc",
@@ -148,6 +149,8 @@ def load() -> ct.CDLL:
         "mcmc_chains_create": (ct.c_int, [P, ct.POINTER(SamplerCfg), i64, i64, u64, dp, pp]),
         "mcmc_chains_destroy": (ct.c_int, [P]),
         "mcmc_chains_reset": (ct.c_int, [P]),
+        "mcmc_chains_set_state": (ct.c_int, [P, dp, dp]),
+        "mcmc_chains_fork": (ct.c_int, [P, i64, i64, pp]),
         "mcmc_chains_steps_done": (ct.c_int, [P, ct.POINTER(i64)]),
         "mcmc_chains_evals": (ct.c_int, [P, ct.POINTER(i64)]),
         "mcmc_chains_ram_factor": (ct.c_int, [P, ct.c_void_p]),

@@ -507,34 +507,75 @@ class _SamplerRunner:
         return _spin(m, self.s, self.r)
 
 
+# ------------------------------------------------------------------ the global random stream
+class _GlobalStream:
+    """The reference's tasks draw their random numbers from Julia's one global RNG as they run, so every spun task
+    -- each element of m * [s1, s2] * r, a second run(m * s * r), the fresh task of resume -- samples a chain of its
+    own (MCMC.jl:87-98, SerialMC.jl:93-97).  Here a chain's stream is the Philox key (seed) and its global chain id
+    (DESIGN.md §3), so the mirror of that global RNG is a seed plus a cursor over chain ids: a task spun by `*` (or
+    resume) takes the next ids when it first runs, exactly as a Julia task first consumes the global RNG when it
+    runs.  srand(seed) restarts the cursor (Julia's srand)."""
+    seed = 1
+    next_chain = 0
+
+
+def srand(seed: int) -> None:
+    """srand(seed) for GPU tasks: later spun tasks draw global chain ids 0, 1, ... under Philox key `seed`."""
+    _GlobalStream.seed = int(seed)
+    _GlobalStream.next_chain = 0
+
+
+def _draw_chains(n: int):
+    """(seed, first global chain id) of n chains taken from the global stream; ids are 32-bit (the Philox counter's
+    chain word), so a cursor that would pass 2^32 moves on to the next key."""
+    n = int(n)
+    if _GlobalStream.next_chain + n > 1 << 32:
+        _GlobalStream.seed += 1
+        _GlobalStream.next_chain = 0
+    first = _GlobalStream.next_chain
+    _GlobalStream.next_chain += n
+    return _GlobalStream.seed, first
+
+
 def _spin(m, s, r):
-    """m * s * r with the reference's array broadcasting (MCMC.jl:87-98)."""
+    """m * s * r with the reference's array broadcasting (MCMC.jl:87-98).  Every task draws its own chains from
+    the global stream when it first runs (seed / chain_offset None until then)."""
     ms = m if isinstance(m, (list, tuple)) else None
     ss = s if isinstance(s, (list, tuple)) else None
     rs = r if isinstance(r, (list, tuple)) else None
     if ms is None and ss is None and rs is None:
-        return MCMCTask(m, s, r)
+        return MCMCTask(m, s, r, seed=None, chain_offset=None)
     n = max(len(x) for x in (ms, ss, rs) if x is not None)
     pick = lambda v, i: v[i] if isinstance(v, (list, tuple)) else v  # noqa: E731
-    return [MCMCTask(pick(m, i), pick(s, i), pick(r, i)) for i in range(n)]
+    return [MCMCTask(pick(m, i), pick(s, i), pick(r, i), seed=None, chain_offset=None) for i in range(n)]
 
 
 class MCMCTask:
-    """A batch of `nchains` independent chains of (model, sampler, runner) on one GPU (MCMC.jl:33-39)."""
+    """A batch of `nchains` independent chains of (model, sampler, runner) on one GPU (MCMC.jl:33-39).
+
+    seed / chain_offset name the chains' random streams (Philox key, first global chain id).  None (tasks spun by
+    `*`): drawn from the global stream when the task first runs (_GlobalStream)."""
 
     def __init__(self, model: MCMCLikelihoodModel, sampler: _Sampler, runner: SerialMC, nchains: int = 1,
-                 seed: int = 1, device: int = 0, chain_offset: int = 0, init_x=None, steps_per_launch: int = 0,
-                 devices: Optional[Sequence[int]] = None):
+                 seed: Optional[int] = 1, device: int = 0, chain_offset: Optional[int] = 0, init_x=None,
+                 steps_per_launch: int = 0, devices: Optional[Sequence[int]] = None):
         self._h = None
         self._group = None
+        self._fork = None            # (batch task, first chain): chains of a batched run(Array), forked on first use
+        self._stopped = False        # prun's tasks (run_serialmc_exit: stop!, SerialMC.jl:87-91)
         if not isinstance(runner, SerialMC) and type(runner).__name__ != "SeqMC":
             raise NotImplementedError("runners: SerialMC (one batch) or SeqMC (lists of targets, run_seqmc)")
         if sampler.uses_gradient and not model.has_gradient:
             name = type(sampler).__name__
             raise AssertionError(f"{name} sampler requires model with gradient function")
         self.model, self.sampler, self.runner = model, sampler, runner
-        self.nchains, self.seed, self.device = int(nchains), int(seed), int(device)
-        self.chain_offset = int(chain_offset)
+        self.nchains, self.device = int(nchains), int(device)
+        self.seed = None if seed is None else int(seed)
+        self.chain_offset = None if chain_offset is None else int(chain_offset)
+        if self.seed is not None and self.chain_offset is None:
+            self.chain_offset = 0
+        if self.seed is None and self.chain_offset is not None:
+            raise ValueError("a task with an explicit chain_offset needs an explicit seed")
         self.init_x = None if init_x is None else np.ascontiguousarray(
             np.asarray(init_x, dtype=np.float64).reshape(model.size, self.nchains))
         self.steps_per_launch = int(steps_per_launch)
@@ -545,15 +586,35 @@ class MCMCTask:
             raise ValueError("devices must list at least one GPU")
 
     def batch(self, nchains: int, seed: Optional[int] = None, **kw) -> "MCMCTask":
-        """Same (model, sampler, runner) over `nchains` chains."""
-        return MCMCTask(self.model, self.sampler, self.runner, nchains=nchains,
-                        seed=self.seed if seed is None else seed, device=kw.get("device", self.device),
-                        chain_offset=kw.get("chain_offset", self.chain_offset), init_x=kw.get("init_x"),
+        """Same (model, sampler, runner) over `nchains` chains.  An explicit seed names the stream outright
+        (chain_offset defaults to 0); without one the new task keeps this task's stream (drawn when it runs, for a
+        spun task)."""
+        off = kw.get("chain_offset", self.chain_offset)
+        if seed is not None and off is None:
+            off = 0
+        if seed is None:
+            seed = self.seed
+            if seed is None and off is not None:
+                seed = _GlobalStream.seed
+        return MCMCTask(self.model, self.sampler, self.runner, nchains=nchains, seed=seed,
+                        device=kw.get("device", self.device), chain_offset=off, init_x=kw.get("init_x"),
                         steps_per_launch=kw.get("steps_per_launch", self.steps_per_launch),
                         devices=kw.get("devices", self.devices))
 
+    def _draw(self) -> None:
+        if self.seed is None:
+            self.seed, self.chain_offset = _draw_chains(self.nchains)
+
     def handle(self) -> ct.c_void_p:
         """The mcmc_chains (one context) or, with `devices`, the mcmc_group_chains of this task."""
+        if self._stopped:
+            raise AssertionError("the task was stopped by prun (run_serialmc_exit, SerialMC.jl:87-91)")
+        if self._h is None and self._fork is not None:             # chains k.. of a batched run: a copy of them
+            src, first = self._fork
+            h = ct.c_void_p()
+            check(_lib.load().mcmc_chains_fork(src.handle(), first, self.nchains, ct.byref(h)))
+            self._h, self._fork = h, None
+        self._draw()
         if self._h is None and self.devices is not None:
             lib = _lib.load()
             g = ct.c_void_p()
@@ -597,7 +658,7 @@ class MCMCTask:
     @property
     def steps_done(self) -> int:
         if self._h is None:
-            return 0
+            return self._fork[0].steps_done if self._fork is not None else 0
         v = ct.c_int64(0)
         if self.devices is not None:
             check(_lib.load().mcmc_group_chains_steps_done(self._h, ct.byref(v)))
@@ -693,6 +754,18 @@ class MCMCChain:
         self.kernel_ms = kernel_ms
         self.final_x, self.final_lp = final_x, final_lp
 
+    def _chains(self, first: int, count: int, task: "MCMCTask") -> "MCMCChain":
+        """Chains [first, first + count) of this result as the result of `task`."""
+        sl = slice(first, first + count)
+        diags = dict(self.diagnostics)
+        diags["accept"] = self.diagnostics["accept"][sl]
+        if "leaps" in diags:
+            diags["leaps"] = {k: v[..., sl] for k, v in self.diagnostics["leaps"].items()}
+        g = None if self._gradients is None else self._gradients[:, :, sl]
+        fx = None if self.final_x is None else self.final_x[:, sl]
+        flp = None if self.final_lp is None else self.final_lp[sl]
+        return MCMCChain(self.range, self._samples[:, :, sl], g, diags, task, self.runTime, self.kernel_ms, fx, flp)
+
     @property
     def samples(self) -> np.ndarray:
         return np.transpose(self._samples, (2, 0, 1))
@@ -776,33 +849,126 @@ def _run_task(t: MCMCTask) -> MCMCChain:
     return MCMCChain(r.r, samples, grads, diags, t, out.runtime_s, out.kernel_ms, fx, flp)
 
 
+def _same_task_kind(t: MCMCTask, t0: MCMCTask) -> bool:
+    """t can share one chain batch with t0: the same model object, sampler configuration and runner, a stream
+    still to be drawn, one context, every chain at model.init."""
+    return (isinstance(t, MCMCTask) and t._h is None and t._fork is None and not t._stopped and t.seed is None
+            and t.model is t0.model and type(t.sampler) is type(t0.sampler)
+            and bytes(t.sampler.cfg()) == bytes(t0.sampler.cfg())
+            and getattr(t.sampler, "storeLeaps", False) == getattr(t0.sampler, "storeLeaps", False)
+            and isinstance(t.runner, SerialMC)
+            and (t.runner.burnin, t.runner.thinning, t.runner.len) == (t0.runner.burnin, t0.runner.thinning,
+                                                                       t0.runner.len)
+            and t.init_x is None and t.devices is None and t0.devices is None and t.device == t0.device
+            and t.steps_per_launch == t0.steps_per_launch)
+
+
+def _run_batched(ts, stop: bool = False, devices=None):
+    """One chain batch for an array of like tasks: the tasks' chains are consecutive global ids drawn from the
+    stream, one mcmc_run_serialmc (or one group run over `devices`) advances them all, and task k's MCMCChain holds
+    its own chains.  Its task then continues them (run(c) = run(c.task), runners.jl:14) from a fork of the batch's
+    state, or, with stop (prun), is stopped as run_serialmc_exit leaves it (SerialMC.jl:87-91)."""
+    t0 = ts[0]
+    n = [t.nchains for t in ts]
+    seed, off = _draw_chains(sum(n))
+    bt = MCMCTask(t0.model, t0.sampler, t0.runner, nchains=sum(n), seed=seed, device=t0.device, chain_offset=off,
+                  steps_per_launch=t0.steps_per_launch, devices=devices)
+    ch = _run_task(bt)
+    out, f = [], 0
+    for t, k in zip(ts, n):
+        t.seed, t.chain_offset = seed, off + f
+        if stop:
+            t._stopped = True
+        else:
+            t._fork = (bt, f)
+        out.append(ch._chains(f, k, t))
+        f += k
+    return out
+
+
 def run(t, *args, nchains: Optional[int] = None, seed: Optional[int] = None, **kw):
-    """run(task) / run(chain) (continue) / run(m, s, r) / run([tasks])  (runners.jl:7-32,45)."""
+    """run(task) / run(chain) (continue) / run(m, s, r) / run([tasks])  (runners.jl:7-32,45).
+
+    run([tasks]) of SerialMC tasks spun by `*` from one model, sampler configuration and runner (m * [s, s] * r,
+    [m, m] * s * r, ...) runs them as ONE chain batch (one launch sequence for all of them); each returned
+    MCMCChain's task continues its own chains.  Other arrays run task by task, as the reference does."""
     if args:                                                 # run(m, s, r)
         return run(_spin(t, args[0], args[1]), nchains=nchains, seed=seed, **kw)
     if isinstance(t, (list, tuple)):
+        if not t:
+            return []
         kinds = {type(x.runner if isinstance(x, MCMCTask) else x.task.runner) for x in t}
         if len(kinds) != 1:
             raise AssertionError("Runners do not have the same runner type")
         if next(iter(kinds)).__name__ == "SeqMC":                 # run(t::Array{MCMCTask}) -> run_seqmc
             from .seqmc import run_seqmc
             return run_seqmc(t, seed=1 if seed is None else seed, **kw)
+        if nchains is None and seed is None and not kw and all(_same_task_kind(x, t[0]) for x in t):
+            return _run_batched(list(t))
         return [run(x, nchains=nchains, seed=seed, **kw) for x in t]
     if isinstance(t, MCMCChain):                              # run(c::MCMCChain) = run(c.task)
         return _run_task(t.task)
     if nchains is not None or seed is not None or kw:
-        if t._h is not None:
+        if t._h is not None or t._fork is not None:
             raise ValueError("task already started; build a new task to change nchains/seed")
         t = t.batch(nchains if nchains is not None else t.nchains, seed=seed, **kw)
     return _run_task(t)
 
 
-def resume(c, steps: int = 100):
-    """resume(chain; steps): a *new* task from model.init with SerialMC(steps, thinning) (SerialMC.jl:93-97)."""
+def prun(t, devices: Optional[Sequence[int]] = None):
+    """prun(tasks) (runners.jl:35-42): pmap(run_serialmc_exit, t) -- every task run to its end, in parallel, then
+    stopped.  Here like tasks form one chain batch over `devices` (default: every visible GPU, as one mcmc_group
+    when there are several; the results do not depend on the device count) and come back stopped; other arrays run
+    task by task."""
+    if isinstance(t, MCMCTask):
+        t = [t]
+    t = list(t)
+    if not t:
+        return []
+    kinds = {type(x.runner) for x in t}
+    if len(kinds) != 1:
+        raise AssertionError("Runners do not have the same runner type")
+    if not isinstance(t[-1].runner, SerialMC):
+        return None                                          # the reference's prun only runs SerialMC tasks
+    if devices is None:
+        nd = device_count()
+        devices = tuple(range(nd)) if nd > 1 else None
+    if all(_same_task_kind(x, t[0]) for x in t):
+        return _run_batched(t, stop=True, devices=devices)
+    out = [_run_task(x) for x in t]
+    for x in t:
+        x._stopped = True
+    return out
+
+
+def resume(c, steps: int = 100, seed: Optional[int] = None, chain_offset: Optional[int] = None):
+    """resume(chain; steps) (SerialMC.jl:93-97): run(t.model, t.sampler, SerialMC(steps, thinning)) -- a *new*
+    task from model.init.  Its chains are drawn from the global stream (the reference's new task samples on from the
+    advanced global RNG), so they are not a replay of the original run; seed / chain_offset name them outright."""
     if isinstance(c, (list, tuple)):
-        return [resume(x, steps=steps) for x in c]
+        return [resume(x, steps=steps, seed=seed, chain_offset=chain_offset) for x in c]
     t = c.task if isinstance(c, MCMCChain) else c
+    if seed is not None and chain_offset is None:
+        chain_offset = 0
+    if seed is None and chain_offset is not None:
+        seed = _GlobalStream.seed
     nt = MCMCTask(t.model, t.sampler, SerialMC(steps=steps, thinning=t.runner.thinning), nchains=t.nchains,
-                  seed=t.seed, device=t.device, chain_offset=t.chain_offset, init_x=t.init_x,
+                  seed=seed, device=t.device, chain_offset=chain_offset, init_x=t.init_x,
                   steps_per_launch=t.steps_per_launch, devices=t.devices)
     return _run_task(nt)
+
+
+def reset(t, x) -> np.ndarray:
+    """MCMC.reset(t::MCMCTask, x) (MCMC.jl:39; the samplers' :reset hooks, RWM.jl:49, MALA.jl:75-80, HMC.jl:114-116,
+    HMCDA.jl:82-83, RAM.jl:47): every chain of the task moves to x ([d], or [d][nchains] per chain) and its
+    log-target (and gradient) is re-evaluated there; step counter, tuners and RAM factor are kept.  Returns the
+    log-targets at x [nchains]."""
+    if t.devices is not None:
+        raise NotImplementedError("reset of a group task: reset its blocks' tasks on one device")
+    h = t.handle()
+    d, C = t.model.size, t.nchains
+    xs = np.asarray(x, dtype=np.float64)
+    xs = np.ascontiguousarray(np.repeat(xs.reshape(d, 1), C, axis=1) if xs.size == d else xs.reshape(d, C))
+    lp = np.empty(C)
+    check(_lib.load().mcmc_chains_set_state(h, dptr(xs), dptr(lp)))
+    return lp

@@ -279,3 +279,50 @@ def test_julia_hook_structs_mirror_header(c_name, hook_name, plain_name):
     c = _c_struct_fields(c_name)
     assert _jl_struct_fields(os.path.join(jdir, "mcmc_jl_hook.jl"), hook_name) == c
     assert _jl_struct_fields(os.path.join(jdir, "MCMCHip.jl"), plain_name) == c
+
+
+def test_julia_hook_defines_batched_runners_reset_ou_and_leaps():
+    """The MCMC.jl hook (Julia 0.3 text, no Julia here): run(::Array{MCMCTask}) and prun(::Array{MCMCTask}) are
+    redefined with the batched GPU path and the reference's dispatch as fallback (runners.jl:17-42), every GPU task
+    installs the :reset hook MCMC.reset calls (MCMC.jl:39), the OU model kind is there, storeLeaps records map into
+    diagnostics["leaps"] as HMCSample arrays, and spun tasks draw their chains from the global stream rather than a
+    fixed seed."""
+    jl = open(os.path.join(ROOT, "mcmc.jl_amd", "julia", "mcmc_jl_hook.jl")).read()
+    for needle in ("function run(t::Array{MCMCTask}; args...)", "function prun(t::Array{MCMCTask}; args...)",
+                   "hip_batchable(t) && return hip_run_tasks(t, false)", "hip_batchable(t) && return hip_run_tasks(t, true)",
+                   "run_seqmc(t; args...)", "pmap(run_serialmc_exit, t)", "run_serialtempmc(t)",
+                   "task_local_storage(:reset,", ":ou => 9", "mcmc_chains_fork", "mcmc_chains_set_state",
+                   'diag["leaps"] = hip_leap_states', 'diags["leaps"]', "HMCSample(", "mcmc_chains_store_leaps",
+                   "hip_draw(1)", "hip_srand", "stop!(res[k])"):
+        assert needle in jl, needle
+    assert "seed = 1\n" not in jl                       # no fixed per-task seed (ADVICE r4)
+    plain = open(os.path.join(ROOT, "mcmc.jl_amd", "julia", "MCMCHip.jl")).read()
+    for needle in ("function ou_model", "MODEL_OU", "mcmc_chains_set_state", "mcmc_chains_fork"):
+        assert needle in plain, needle
+
+
+def test_spun_tasks_draw_from_the_global_stream():
+    """m * s * r tasks carry no stream until they run; srand restarts the cursor; draws are consecutive and move to
+    the next key before the 32-bit chain id would overflow; explicit seeds keep offset 0 (host logic only)."""
+    from mcmchip import api
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(3), grad=True)
+    r = mc.SerialMC(steps=10)
+    t = m * mc.RWM(0.1) * r
+    assert t.seed is None and t.chain_offset is None
+    ts = m * [mc.RWM(0.1), mc.RWM(0.1)] * r
+    assert all(x.seed is None for x in ts) and api._same_task_kind(ts[1], ts[0])
+    assert not api._same_task_kind((m * mc.MALA(0.1) * r), ts[0])
+    assert not api._same_task_kind((m * mc.RWM(0.2) * r), ts[0])
+    mc.srand(5)
+    assert api._draw_chains(3) == (5, 0) and api._draw_chains(2) == (5, 3)
+    api._GlobalStream.next_chain = (1 << 32) - 1
+    assert api._draw_chains(2) == (6, 0)
+    mc.srand(9)
+    b = t.batch(64)
+    assert b.seed is None and b.chain_offset is None
+    b._draw()
+    assert (b.seed, b.chain_offset) == (9, 0) and api._GlobalStream.next_chain == 64
+    e = t.batch(64, seed=3)
+    assert (e.seed, e.chain_offset) == (3, 0)
+    with pytest.raises(ValueError):
+        mc.MCMCTask(m, mc.RWM(0.1), r, seed=None, chain_offset=4)

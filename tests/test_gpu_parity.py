@@ -268,10 +268,17 @@ def test_single_chain_readme_example(gpu):
 
 
 def test_resume_restarts_from_init(gpu):
+    """resume (SerialMC.jl:93-97) spins a new task from model.init whose chains come from the global stream: not a
+    replay of the original run's first steps, but bitwise the oracle's chains at the ids it drew."""
     m = _model("iso", 3)
     ch = mc.run((m * mc.RWM(0.5) * mc.SerialMC(steps=20, thinning=2)).batch(64, seed=9))
     ch2 = mc.resume(ch, steps=30)
     assert ch2.samples.shape == (64, 15, 3) and ch2.task.steps_done == 30
+    t2 = ch2.task
+    oc = orc.OracleChains(m, mc.RWM(0.5), nchains=64, seed=t2.seed, chain_offset=t2.chain_offset)
+    s_ref, g_ref, acc_ref = oc.run(mc.SerialMC(steps=30, thinning=2))
+    assert_parity(ch2, s_ref, g_ref, acc_ref, "rwm")
+    assert not np.array_equal(ch2._samples[:10], ch._samples[:10])     # a fresh stream, not the original's
 
 
 @pytest.mark.parametrize("d", [9, 300])
@@ -804,6 +811,24 @@ def test_ou_example_runs_bitwise(gpu):
     chain = mc.run((m * mc.RAM() * r).batch(1, seed=1))
     tail = chain._samples[5000:, :, 0].mean(axis=0)
     assert abs(tail[2] - 10.0) < 0.5 and abs(tail[0] - 20.0) < 8.0 and abs(tail[1] - 0.1) < 0.02, tail
+
+
+@pytest.mark.parametrize("C", [1, 5])
+def test_ou_few_chain_rwm_bitwise(gpu, C):
+    """RWM on the joint OU target with one chain (the path-speculation kernel lpc_rwm_spec, chosen for C == 1) and
+    with a few chains (lpc_rwm_la): the joint log-target, not a per-coordinate sum, decides every step (ADVICE r4:
+    a per-coordinate sum of a joint model is 0 and accepted every proposal), bitwise against the oracle."""
+    m = _ou_model()
+    r = mc.SerialMC(steps=400, burnin=50, thinning=7)
+    task = (m * mc.RWM(0.05) * r).batch(C, seed=41)
+    chain = mc.run(task)
+    assert task.step_kernel.startswith("lpc_rwm_spec" if C == 1 else "lpc_rwm_la"), task.step_kernel
+    oc = orc.OracleChains(m, mc.RWM(0.05), nchains=C, seed=41)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref, acc_ref, "rwm")
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    acc = chain.diagnostics["accept"]
+    assert 0 < acc.sum() < acc.size                           # some proposals rejected (out of support, or worse)
 
 
 def test_ou_eval_and_limits(gpu):

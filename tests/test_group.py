@@ -105,7 +105,9 @@ def test_group_equals_one_context(gpu, case, devices):
         assert np.array_equal(task.ram_factor().view(np.uint64), one.task.ram_factor().view(np.uint64))
     # continue (run(chain), runners.jl:14) and resume (SerialMC.jl:93-97) on the group
     _same(mc.run(grp), mc.run(one))
-    _same(mc.resume(grp, steps=7), mc.resume(one, steps=7))
+    _same(mc.resume(grp, steps=7, seed=11, chain_offset=4096), mc.resume(one, steps=7, seed=11, chain_offset=4096))
+    a, b = mc.resume(grp, steps=7), mc.resume(one, steps=7)          # each draws its own chains from the stream
+    assert a.task.chain_offset != b.task.chain_offset and not np.array_equal(a._samples, b._samples)
 
 
 @pytest.mark.gpu
