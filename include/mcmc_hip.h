@@ -329,7 +329,8 @@ int mcmc_stats_ess(mcmc_ctx* ctx, const double* samples, int64_t nkept, int64_t 
  *      8 accept uniform, 9 Box-Muller radius log, 10/11 Box-Muller angle sin/cos,
  *      12 guard-free sqrt of the Box-Muller radius, 13/14 det_exp_tab / det_log_tab, 15 the screened accept test,
  *      16 the Box-Muller radius^2 -2 log u (bm_rad2_u32, bitwise -2 x op 9), 17 the Box-Muller radius
- *      sqrt(-2 log u) (bm_radius_u32, the segment polynomials). ---- */
+ *      sqrt(-2 log u) (bm_radius_u32, the segment polynomials), 22 / 23 the logistic Bernoulli term / its
+ *      eta-derivative weight of (eta = x, w = y) (det_logi). ---- */
 int mcmc_debug_detmath(mcmc_ctx* ctx, int op, int64_t n, const double* x, const double* y, double* out);
 int mcmc_debug_philox(mcmc_ctx* ctx, int64_t n, const uint32_t* ctr /*[n][4]*/, const uint32_t* key /*[n][2]*/,
                       uint32_t* out /*[n][4]*/);

@@ -20,6 +20,7 @@
 
 #include "bm_log_table.inc"
 #include "erfc_table.inc"
+#include "softplus_table.inc"
 
 namespace mcmc {
 
@@ -494,6 +495,73 @@ __device__ __forceinline__ double det_log_tab(double v, const double (*tab)[4] =
     det_log_tab_s1(v, L, tab);
     det_log_tab_s2(L);
     return det_log_tab_fin(L);
+}
+
+// The logistic Bernoulli term of one observation (examples/logistic_regression.jl:19-21) and its eta-derivative
+// (MCMCDerivRules.jl:111): lp = logpdf(Bernoulli(p), y), p = 1/(1+exp(-s eta)) (s = the link sign), and
+// s (y - p).  The staged tile carries w = s (2y - 1) instead of y (glm_layout.hpp); with u = -w eta
+//     lp = -softplus(u) = -(max(u, 0) + f(|u|)),          f(v) = log1p(exp(-v)),
+//     s (y - p) = w sigmoid(u) = w (u >= 0 ? 1 - g : g),  g(v) = 1/(1+exp(v)) = -f'(v).
+// v = min(|u|, 40) splits as j/8 + t (|t| <= 1/16, j from the low word of a shifter fma, t exact) and row j of
+// kSoftplusTab holds the degree-9 polynomial of f in t (Chebyshev interpolation, scripts/gen_softplus_table.py): one
+// Horner pass with derivative gives f = P(t) (<= 1.4 ulp) and g = -P'(t) (<= 1.9 ulp).  No exp, log or division.
+// Beyond v = 40, f and g (< 4.3e-18) keep their v = 40 values.  The reference's own arithmetic (p rounded, then
+// log(p) or log(1 - p)) makes the term -Inf where p rounds to 1 with y = 0 or to 0 with y = 1: u >= T(y)
+// (glm_layout.hpp logi_bound).  The kernels keep that: the tile carries b = -T(y) beside w and a lane whose max of u + b over its
+// observations is >= 0 contributes -Inf, so LLAcc puts the point out of support exactly where the reference does.
+// A NaN eta is not propagated (fmin): it needs a NaN or overflowing X beta, whose prior term already puts the chain
+// out of support (glm_finish; X and Y are finite by mcmc_model_create).  Stages as det_exp (the caller interleaves
+// work between them); oracle twin orc_logi.
+static __device__ const double kSoftplusTab[SP_NROWS][10] = {SP_TABLE_ROWS};
+
+
+struct LogiState {
+    double u, t, p, d;
+    const dm_f64x2* row;
+};
+__device__ __forceinline__ void det_logi_s1(double eta, double w, LogiState& S, const double (*tab)[10] = kSoftplusTab) {
+    const double shifter = 0x1.8p52;
+    const double u = -(w * eta);
+    const double vs = __builtin_fmin(__builtin_fabs(u), (double)SP_VMAX);
+    const double tt = __builtin_fma(vs, (double)SP_SEG, shifter);           // 1.5 2^52 + j, j = round(8 v)
+    const uint32_t j = (uint32_t)d2bits(tt);                                   // in [0, 320]
+    const double kd = tt - shifter;
+    S.t = __builtin_fma(-kd, 1.0 / SP_SEG, vs);                                // exact
+    S.row = reinterpret_cast<const dm_f64x2*>(tab[j]);
+    S.u = u;
+}
+// Horner with derivative over c9 .. c5
+__device__ __forceinline__ void det_logi_s2(LogiState& S) {
+    const double t = S.t;
+    const dm_f64x2 c89 = S.row[4], c67 = S.row[3], c45 = S.row[2];
+    double p = c89.y, d = c89.y;
+    p = __builtin_fma(p, t, c89.x);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c67.y);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c67.x);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c45.y);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c45.x);
+    S.p = p;
+    S.d = d;
+}
+// c4 .. c0, then the term and the weight
+__device__ __forceinline__ void det_logi_fin(const LogiState& S, double w, double& term, double& rv) {
+    const double t = S.t;
+    const dm_f64x2 c23 = S.row[1], c01 = S.row[0];
+    double p = S.p, d = S.d;
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c23.y);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c23.x);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c01.y);
+    d = __builtin_fma(d, t, p); p = __builtin_fma(p, t, c01.x);
+    term = -(__builtin_fmax(S.u, 0.0) + p);                                   // -softplus(u)
+    const double sig = S.u >= 0.0 ? 1.0 + d : -d;                              // 1 - g or g
+    rv = w * sig;
+}
+__device__ __forceinline__ void det_logi(double eta, double w, double& term, double& rv,
+                                         const double (*tab)[10] = kSoftplusTab) {
+    LogiState S;
+    det_logi_s1(eta, w, S, tab);
+    det_logi_s2(S);
+    det_logi_fin(S, w, term, rv);
 }
 
 // sin, cos of 2 pi w 2^-32 (the Box-Muller angle), table-driven: the angle splits as k/1024 + j 2^-32 turns

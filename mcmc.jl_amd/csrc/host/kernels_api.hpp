@@ -56,7 +56,7 @@ hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t 
 int mcmc_glm_d_pad(int d);
 // the regression kernels' staged-tile image of X and Y (glm_layout.hpp): its size in doubles, and the packing
 size_t mcmc_glm_image_doubles(int d, int64_t n);
-void mcmc_glm_pack_image(int d, int64_t n, const double* X, const double* Y, double* img);
+void mcmc_glm_pack_image(int d, int64_t n, const double* X, const double* Y, const double* B, double* img);
 // steps one launch of the regression step kernel may fuse (0: any)
 int mcmc_glm_steps_per_launch(int d, int64_t n, int sampler_kind);
 

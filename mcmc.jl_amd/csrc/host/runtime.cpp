@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../../include/mcmc_hip.h"
+#include "../glm_layout.hpp"
 #include "../common.hpp"
 #include "internal.hpp"
 #include "kernels_api.hpp"
@@ -416,7 +417,23 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
             // each tile, zero padding), plus Y [n_pad] on its own
             const int64_t n_pad = (desc->n + 15) / 16 * 16;
             std::vector<double> Xp(mcmc_glm_image_doubles((int)d, desc->n)), Yp((size_t)n_pad, 0.0);
-            mcmc_glm_pack_image((int)d, desc->n, desc->X, desc->Y, Xp.data());
+            for (int64_t i = 0; i < desc->n * (int64_t)d; ++i)
+                if (!std::isfinite(desc->X[i])) return bail(fail(MCMC_E_INVALID_ARG, "X must be finite"));
+            for (int64_t i = 0; i < desc->n; ++i)
+                if (!std::isfinite(desc->Y[i])) return bail(fail(MCMC_E_INVALID_ARG, "Y must be finite"));
+            // the logistic model's tile columns hold w = s (2y - 1) (s the link sign) instead of y and the bounds
+            // -T(y) where the reference's p rounds to 1 or 0 (detmath.hpp det_logi, logi_bound)
+            std::vector<double> Yw, Bw;
+            if (desc->kind == MCMC_MODEL_LOGISTIC) {
+                Yw.resize((size_t)desc->n);
+                Bw.resize((size_t)desc->n);
+                for (int64_t i = 0; i < desc->n; ++i) {
+                    Yw[(size_t)i] = desc->Y[i] == 1.0 ? desc->link_sign : -desc->link_sign;
+                    Bw[(size_t)i] = mcmc::logi_bound(desc->Y[i]);
+                }
+            }
+            mcmc_glm_pack_image((int)d, desc->n, desc->X, Yw.empty() ? desc->Y : Yw.data(),
+                                Bw.empty() ? nullptr : Bw.data(), Xp.data());
             for (int64_t i = 0; i < desc->n; ++i) Yp[(size_t)i] = desc->Y[i];
             if (int r = dmalloc(&m->d_X, Xp.size())) return bail(r);
             if (int r = dmalloc(&m->d_Y, Yp.size())) return bail(r);

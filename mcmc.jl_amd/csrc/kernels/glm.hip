@@ -120,8 +120,8 @@ __device__ __forceinline__ int own_coord(const GlmPos& p, int slot) {
 // tile's last reader, behind a barrier)
 __host__ __device__ constexpr int glm_xbufs(int nw, int d_pad) { return nw == 1 ? 3 : (d_pad > 512 ? 1 : 2); }
 
-// LDS carve-up (doubles): tiles [xbufs][ts] | eta partials [8 waves][64][4] | chain scalars [8 waves][16] |
-// residual weights [4 tiles][4][64] | int scratch
+// LDS carve-up (doubles): tiles [xbufs][ts] | eta partials [8 waves][64][4] (single-slice kernels: the logistic
+// term's table, kSoftplusTab, instead) | chain scalars [8 waves][16] | residual weights [4 tiles][4][64] | int scratch
 struct GlmLds {
     double* X;
     double* part;
@@ -131,11 +131,15 @@ struct GlmLds {
     double* beta;     // single-slice kernels: [4 waves][4 NM slots][64 lanes], a lane's proposal coordinates
 };
 
+__host__ __device__ constexpr int glm_part_doubles(int nw) {
+    return nw == 1 && SP_NROWS * 10 > kGlmMaxWaves * 64 * 4 ? SP_NROWS * 10 : kGlmMaxWaves * 64 * 4;
+}
+
 __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
     GlmLds L;
     L.X = smem;
     L.part = L.X + glm_xbufs(a.g.nw, a.g.d_pad) * a.g.ts;                 // tile buffers
-    L.scal = L.part + kGlmMaxWaves * 64 * 4;
+    L.scal = L.part + glm_part_doubles(a.g.nw);
     L.rbuf = L.scal + kGlmMaxWaves * 16;
     L.iscr = (int*)(L.rbuf + 4 * 4 * 64);
     L.beta = L.rbuf + 4 * 4 * 64 + 2;                // after the 4 ints of iscr
@@ -143,7 +147,7 @@ __device__ __forceinline__ GlmLds glm_lds(const GlmArgs& a, double* smem) {
 }
 
 static size_t glm_lds_bytes(const GlmShape& g) {
-    return (size_t)(glm_xbufs(g.nw, g.d_pad) * g.ts + kGlmMaxWaves * 64 * 4 + kGlmMaxWaves * 16 +
+    return (size_t)(glm_xbufs(g.nw, g.d_pad) * g.ts + glm_part_doubles(g.nw) + kGlmMaxWaves * 16 +
                     4 * 4 * 64 + 2 + (g.nw == 1 ? 4 * 4 * g.nm * 64 : 0)) * 8
 #ifdef GLM_STAMP
            + 16 + (g.nw > 1 ? kGlmStampLdsBytes : 0)
@@ -249,7 +253,6 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
     constexpr int S = glm_row_stride(16 * NM);
-    const double sgn = M.link_sign;
     const bool probit = !LOGI && M.kind == MK_PROBIT;          // probit runs in the linear instantiation (uniform)
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = LOGI ? 0.0 : det_log(sn);
@@ -260,6 +263,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
     constexpr int DP = 16 * NM;
     constexpr int XS = glm_tile_doubles(DP);                  // one staged tile: X rows, then Y
     constexpr int YO = glm_y_offset(DP);
+    constexpr int BO = glm_b_offset(DP);
     constexpr int kHalf = XS / 2;                             // f64x2 per tile
     constexpr int kPer = (kHalf + kBlk - 1) / kBlk;
     static_assert(glm_row_stride(DP) > 0, "");
@@ -297,13 +301,11 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         load_tile(1);
         store_tile(1);
     }
-    // logistic: the exp / log tables (det_exp_tab, det_log_tab) staged in the eta-partials area, which the
+    // logistic: the term's segment-polynomial table (det_logi) staged in the eta-partials area, which the
     // single-slice kernels do not otherwise use
-    const double (*ltab)[4] = reinterpret_cast<const double (*)[4]>(L.part);
-    const double (*etab)[2] = reinterpret_cast<const double (*)[2]>(L.part + 4 * 128);
+    const double (*sptab)[10] = reinterpret_cast<const double (*)[10]>(L.part);
     if (LOGI) {
-        for (int i = threadIdx.x; i < 4 * 128 + 2 * 64; i += kBlk)
-            L.part[i] = i < 4 * 128 ? (&kBmLogTab[0][0])[i] : (&kExp2Tab[0][0])[i - 4 * 128];
+        for (int i = threadIdx.x; i < SP_NROWS * 10; i += kBlk) L.part[i] = (&kSoftplusTab[0][0])[i];
     }
     if (GRAD) {
 #pragma unroll
@@ -311,6 +313,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
     }
     __syncthreads();
     f64x4 eta = eta_of(0);
+    double ubnd = -__builtin_inf();                           // logistic: max of u + b over the lane's observations
     const int64_t nfull = M.n / 16;                           // tiles without padded observations
     int b = 0;                                                // buffer of tile t
     for (int64_t t = 0; t < ntiles; ++t) {
@@ -328,17 +331,21 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         f64x4 eta_next = f64x4{0.0, 0.0, 0.0, 0.0};
         const double* xrow1 = L.X + b1 * XS + eta_lane;
         const double* LY = L.X + b * XS + YO;
+        const double* LB = L.X + b * XS + BO;
         double av[KM];
 #pragma unroll
         for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow1[glm_eta_off(m)];
-        double y[4], pr[4], term[4], rv[4];
-        ExpTState E[4];
-        LogTState Lg[4];
+        double y[4], bnd[4], term[4], rv[4];                    // y: the response, for the logistic model w (det_logi)
+        LogiState E[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
+        if (LOGI) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bnd[r] = LB[p.q + 4 * r];
+        }
         // sub-stage j: the eta MFMAs [j KM / NSUB, (j+1) KM / NSUB), then stage st of one row (kGlmGroupRows
         // false) or of all four rows, four independent dependency chains (kGlmGroupRows true)
-        constexpr int NSTAGE = LOGI ? 6 : 1;
+        constexpr int NSTAGE = LOGI ? 3 : 1;
         constexpr int NSUB = kGlmGroupRows ? NSTAGE : 4 * NSTAGE;
 #pragma unroll
         for (int j = 0; j < NSUB; ++j) {
@@ -352,16 +359,14 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
             for (int r = 0; r < 4; ++r) {
                 if (!kGlmGroupRows && r != (j & 3)) continue;
                 if (LOGI) {
+                    // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111)
                     switch (st) {
-                        case 0: det_exp_tab_s1(-(sgn * eta[r]), E[r], etab); break;     // prob = 1/(1+exp(-X*vars))
-                        case 1: det_exp_tab_s2(E[r]); break;
-                        case 2: pr[r] = 1.0 / (1.0 + det_exp_tab_fin(E[r])); break;
-                        case 3: det_log_tab_s1((y[r] >= 0.5) ? pr[r] : 1.0 - pr[r], Lg[r], ltab); break;  // Y ~ Bernoulli
-                        case 4: det_log_tab_s2(Lg[r]); break;
-                        default:
-                            term[r] = det_log_tab_fin(Lg[r]);
-                            rv[r] = sgn * (y[r] - pr[r]);                           // MCMCDerivRules.jl:111, closed form
+                        case 0:
+                            det_logi_s1(eta[r], y[r], E[r], sptab);
+                            ubnd = __builtin_fmax(ubnd, E[r].u + bnd[r]);            // the reference's -Inf
                             break;
+                        case 1: det_logi_s2(E[r]); break;
+                        default: det_logi_fin(E[r], y[r], term[r], rv[r]); break;
                     }
                 } else if (probit) {
                     glm_probit_obs(eta[r], y[r], term[r], rv[r]);
@@ -413,7 +418,7 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         eta = eta_next;
         b = b1;
     }
-    return lik_part;
+    return LOGI && ubnd >= 0.0 ? -__builtin_inf() : lik_part;
 }
 
 template <int NM, bool GRAD, class XA>
@@ -512,9 +517,9 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     constexpr int S = glm_row_stride(DP);
     constexpr int XS = glm_tile_doubles(DP);
     constexpr int YO = glm_y_offset(DP);
+    constexpr int BO = glm_b_offset(DP);
     constexpr bool kOneBuf = DP > 512;                        // glm_xbufs: one LDS tile buffer
     const bool logistic = M.kind == MK_LOGISTIC;
-    const double sgn = M.link_sign;
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = logistic ? 0.0 : det_log(sn);
     const double isn = 1.0 / sn, is2n = 1.0 / s2n;
@@ -523,6 +528,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
     }
     double lik_part = 0.0;
+    double ubnd = -__builtin_inf();                           // logistic: max of u + b over the lane's observations
     const int64_t ntiles = g.n_pad / 16;
     const int eta_lane = p.cl * S + 4 * p.q + p.base;                       // + glm_eta_off(slot)
     const int g_lane = p.q * S + 4 * (p.cl & 3) + (p.cl >> 2) + p.base;   // + 4 kk S + glm_g_off(T)
@@ -547,9 +553,13 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         constexpr int RPW = NW >= 4 ? 1 : 4 / NW;
         const int r0 = p.slice * RPW;
         const double* LY = LX + YO;
-        double yv[RPW];
+        double yv[RPW], bv[RPW];
 #pragma unroll
         for (int rr_ = 0; rr_ < RPW; ++rr_) yv[rr_] = LY[p.q + 4 * ((r0 + rr_) & 3)];
+        if (logistic) {
+#pragma unroll
+            for (int rr_ = 0; rr_ < RPW; ++rr_) bv[rr_] = LX[BO + p.q + 4 * ((r0 + rr_) & 3)];
+        }
         f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
         {
             constexpr int KM = 4 * NM;
@@ -600,10 +610,12 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             const double y = yv[rr_];
             double term, w;
             if (logistic) {
-                const double tt = det_exp_tab(-(sgn * e));              // prob = 1/(1+exp(-X*vars))
-                const double pr = 1.0 / (1.0 + tt);
-                term = det_log_tab((y >= 0.5) ? pr : 1.0 - pr);         // Y ~ Bernoulli(prob)
-                w = sgn * (y - pr);                                     // MCMCDerivRules.jl:111 chain, closed form
+                // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); MCMCDerivRules.jl:111 (y: the image's w, det_logi)
+                LogiState E;
+                det_logi_s1(e, y, E);
+                ubnd = __builtin_fmax(ubnd, E.u + bv[rr_]);                  // the reference's -Inf (logi_bound)
+                det_logi_s2(E);
+                det_logi_fin(E, y, term, w);
             } else if (M.kind == MK_PROBIT) {
                 glm_probit_obs(e, y, term, w);
             } else {
@@ -666,7 +678,8 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     if (blockIdx.x < 4 && (threadIdx.x & 63) == 0)
         for (int j = 0; j < 16 * 8; ++j) (&g_glm_stamps[blockIdx.x][threadIdx.x >> 6][0][0])[j] = stamp_lds[(threadIdx.x >> 6) * 128 + j];
 #endif
-    return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, lik_part, oos);
+    return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, logistic && ubnd >= 0.0 ? -__builtin_inf() : lik_part,
+                                    oos);
 }
 
 // ------------------------------------------------------------------ state access (layout [d][ld])
@@ -1187,7 +1200,8 @@ __global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
 // over (m, e, q); G chains over observations; a lane's likelihood terms in (t, r) order; qf / qb / prior as
 // there), so the results are glm_mala1's bit for bit and orc_glm_eval restates them.
 // LDS (doubles; XS = glm_tile_doubles(16 NM), X rows then Y): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
-// which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | tables | qf, lik [2][4][16].
+// which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | the logistic term's table
+// (kSoftplusTab) | qf, lik [2][4][16].
 template <int NM>
 __host__ __device__ constexpr int glm_ws_region(int XS) {
     return (2 * XS + 4096) > (4 * 4 * NM * 64) ? (2 * XS + 4096) : (4 * 4 * NM * 64);
@@ -1195,7 +1209,7 @@ __host__ __device__ constexpr int glm_ws_region(int XS) {
 __host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
     const int XS = glm_tile_doubles(16 * nm);
     const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
-    return (size_t)(2 * XS + R + 4 * 16 + 4 * 128 + 2 * 64 + 2 * 4 * 16);
+    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16);
 }
 template <int NM>
 __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
@@ -1221,14 +1235,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     constexpr int S = glm_row_stride(16 * NM);
     constexpr int XS = glm_tile_doubles(16 * NM);             // one staged tile: X rows, then Y
     constexpr int YO = glm_y_offset(16 * NM);
+    constexpr int BO = glm_b_offset(16 * NM);
     double* const Xs = smem;                                   // 4 X tile slots: 0, 1 here, 2, 3 in region R
     double* const R = smem + 2 * XS;
     double* const Eb = R + 2 * XS;                             // eta [2][4 tiles][64 lanes][4]
     double* const Rb = Eb + 2048;                              // r   [2][4 tiles][64 lanes][4]
     double* const beta = R;                                    // proposal [4 tiles][NS][64] (proposal phase only)
     double* const Yb = R + glm_ws_region<NM>(XS);              // (unused: Y travels inside each staged tile)
-    double* const ltabp = Yb + 64;                             // logistic tables: log [128][4], exp [64][2]
-    double* const qfl = ltabp + 4 * 128 + 2 * 64;              // qf [4][16], then lik [4][16]
+    double* const ltabp = Yb + 64;                             // logistic term's table [SP_NROWS][10]
+    double* const qfl = ltabp + SP_NROWS * 10;                 // qf [4][16], then lik [4][16]
     double* const likl = qfl + 64;
     auto xslot = [&](int64_t tt) -> double* { const int b = (int)(tt & 3); return b < 2 ? Xs + b * XS : R + (b - 2) * XS; };
     const Stream rs{s.key0, s.key1};
@@ -1295,8 +1310,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         qf = glm_sum(a, p, GlmLds{}, qf);
         if (p.q == 0) qfl[p.tile * 16 + p.cl] = qf;
         if (logi) {
-            for (int e = u; e < 4 * 128 + 2 * 64; e += 256)
-                ltabp[e] = e < 4 * 128 ? (&kBmLogTab[0][0])[e] : (&kExp2Tab[0][0])[e - 4 * 128];
+            for (int e = u; e < SP_NROWS * 10; e += 256) ltabp[e] = (&kSoftplusTab[0][0])[e];
         }
     } else {
         load_tile(0);
@@ -1359,16 +1373,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     if (!vwave) Eq[0] = eta_of(0);
     __syncthreads();
     // ---- the observation tiles
-    const double sgn = M.link_sign;
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = logi ? 0.0 : det_log(sn);
     const double isn = 1.0 / sn, is2n = 1.0 / s2n;
-    const double (*ltab)[4] = reinterpret_cast<const double (*)[4]>(ltabp);
-    const double (*etab)[2] = reinterpret_cast<const double (*)[2]>(ltabp + 4 * 128);
+    const double (*sptab)[10] = reinterpret_cast<const double (*)[10]>(ltabp);
     const int64_t nfull = M.n / 16;
     // one loop per role, each with one barrier per tile (the same count): the roles' loop invariants (the V waves'
     // polynomial constants, the M waves' operand addresses) stay out of each other's register pressure
     double lik_part = 0.0;
+    double ubnd = -__builtin_inf();                            // logistic: max of u + b over the lane's observations
     if (!vwave) {
         for (int64_t t = 0; t < ntiles; ++t) {
             if (t + 1 < ntiles) Eq[256 * ((t + 1) & 1)] = eta_of(t + 1);
@@ -1383,27 +1396,22 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
             }
             const f64x4 eta = Eq[256 * (t & 1)];
             const double* LY = xslot(t) + YO;
-            double y[4], pr[4], term[4], rv[4];
+            double y[4], term[4], rv[4];                       // y: the response, for the logistic model w (det_logi)
 #pragma unroll
             for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
             if (logi) {
-                ExpTState E[4];
-                LogTState Lg[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) det_exp_tab_s1(-(sgn * eta[r]), E[r], etab);   // prob = 1/(1+exp(-X*vars))
-#pragma unroll
-                for (int r = 0; r < 4; ++r) det_exp_tab_s2(E[r]);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) pr[r] = 1.0 / (1.0 + det_exp_tab_fin(E[r]));
-#pragma unroll
-                for (int r = 0; r < 4; ++r) det_log_tab_s1((y[r] >= 0.5) ? pr[r] : 1.0 - pr[r], Lg[r], ltab);   // Y ~ Bernoulli
-#pragma unroll
-                for (int r = 0; r < 4; ++r) det_log_tab_s2(Lg[r]);
+                // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111)
+                const double* LB = xslot(t) + BO;
+                LogiState E[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    term[r] = det_log_tab_fin(Lg[r]);
-                    rv[r] = sgn * (y[r] - pr[r]);                                  // MCMCDerivRules.jl:111, closed form
+                    det_logi_s1(eta[r], y[r], E[r], sptab);
+                    ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * r]);           // the reference's -Inf
                 }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) det_logi_s2(E[r]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) det_logi_fin(E[r], y[r], term[r], rv[r]);
             } else if (M.kind == MK_PROBIT) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) glm_probit_obs(eta[r], y[r], term[r], rv[r]);
@@ -1432,7 +1440,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         }
     }
     if (vwave) {
-        const double lik = glm_sum(a, p, GlmLds{}, lik_part);
+        const double lik = glm_sum(a, p, GlmLds{}, logi && ubnd >= 0.0 ? -__builtin_inf() : lik_part);
         if (p.q == 0) likl[p.tile * 16 + p.cl] = lik;
     } else {
         g_of(ntiles - 1);
@@ -1803,17 +1811,20 @@ size_t mcmc_glm_image_doubles(int d, int64_t n) {
 
 // the staged-tile image of X [n][d] (row-major) and Y [n] (glm_layout.hpp): tile t = rows 16t..16t+15 at
 // positions glm_pos(k) of stride S, then Y; zeros elsewhere (padded rows, coordinates k >= d, gaps)
-void mcmc_glm_pack_image(int d, int64_t n, const double* X, const double* Y, double* img) {
+void mcmc_glm_pack_image(int d, int64_t n, const double* X, const double* Y, const double* B, double* img) {
     const mcmc::GlmShape g = mcmc_glm_shape(d, n);
     const size_t total = mcmc_glm_image_doubles(d, n);
     for (size_t i = 0; i < total; ++i) img[i] = 0.0;
-    const int S = g.lds_stride, YO = mcmc::glm_y_offset(g.d_pad);
+    const int S = g.lds_stride, YO = mcmc::glm_y_offset(g.d_pad), BO = mcmc::glm_b_offset(g.d_pad);
     for (int64_t i = 0; i < n; ++i) {
         double* tile = img + (size_t)(i / 16) * (size_t)g.ts;
         const int r = (int)(i % 16);
         for (int k = 0; k < d; ++k) tile[r * S + k] = X[(size_t)i * d + k];
         tile[YO + r] = Y[i];
+        tile[BO + r] = B ? B[i] : 0.0;
     }
+    if (B)
+        for (int64_t i = n; i < g.n_pad; ++i) img[(size_t)(i / 16) * (size_t)g.ts + BO + (int)(i % 16)] = -HUGE_VAL;
 }
 
 template <int NM, int NW>

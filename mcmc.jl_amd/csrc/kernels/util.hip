@@ -92,6 +92,8 @@ __global__ void k_detmath(int op, int64_t n, const double* x, const double* y, d
         case 18: r = det_erfc(a); break;                           // probit model: erfc, log1p, normal log-cdf
         case 19: r = det_log1p(a); break;
         case 20: r = det_normlogcdf(a); break;
+        case 22: { double tm, rv; det_logi(a, y[i], tm, rv); r = tm; } break;   // logistic term of (eta, w)
+        case 23: { double tm, rv; det_logi(a, y[i], tm, rv); r = rv; } break;   // ... and its weight
         default: r = 0.0;
     }
     out[i] = r;

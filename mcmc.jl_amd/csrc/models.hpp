@@ -191,8 +191,9 @@ struct OUDSL {
     }
     template <int NC>
     __device__ __forceinline__ double joint_lp(const double (&v)[NC], bool& oos) const {
-        const double tau = v[0], sigma = v[1], mu = v[2];
         oos = true;
+        if constexpr (NC < 3) return -__builtin_inf();   // never run: the runtime refuses d != 3 (lpc_rwm_spec<1|2>)
+        const double tau = v[0], sigma = v[1 < NC ? 1 : 0], mu = v[2 < NC ? 2 : 0];
         if (!in_support(tau, sigma, mu)) return -__builtin_inf();
         const double fac = det_exp(-1.0 / tau);
         const double c = mu * (1.0 - fac);
@@ -211,6 +212,7 @@ struct OUDSL {
     }
     template <int NC>
     __device__ __forceinline__ void joint_grad(const double (&v)[NC], double (&g)[NC]) const {
+        static_assert(NC >= 3, "the OU model has 3 parameters");
         const double tau = v[0], sigma = v[1], mu = v[2];
         const double fac = det_exp(-1.0 / tau);
         const double c = mu * (1.0 - fac);

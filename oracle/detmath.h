@@ -32,6 +32,7 @@
 
 #include "bm_log_table.inc"
 #include "erfc_table.inc"
+#include "softplus_table.inc"
 
 #define ORC_PHILOX_M0 0xD2511F53u
 #define ORC_PHILOX_M1 0xCD9E8D57u
@@ -278,6 +279,33 @@ static inline double orc_log_tab(double v) {
     double lo = fma(de, ln2_lo, row[2]) + p;
     double res = v == 0.0 ? -INFINITY : hi + lo;
     return v != v ? v : res;
+}
+
+/* The logistic Bernoulli term and its eta-derivative (examples/logistic_regression.jl:19-21, MCMCDerivRules.jl:111),
+   w = s (2y - 1) (s the link sign), u = -w eta:  term = -(max(u, 0) + f(|u|)), f(v) = log1p(exp(-v)), and
+   rv = w (u >= 0 ? 1 - g : g), g = -f'(v); v = min(|u|, 40) = j/8 + t, f = P_j(t) and f' = P_j'(t) from row j of the
+   generated degree-9 segment polynomials (scripts/gen_softplus_table.py), one Horner pass with derivative in the
+   device's order.  Device twin: det_logi (csrc/detmath.hpp). */
+static const double orc_softplus_tab[SP_NROWS][10] = {SP_TABLE_ROWS};
+
+static inline void orc_logi(double eta, double w, double* term, double* rv) {
+    const double shifter = 0x1.8p52;
+    const double u = -(w * eta);
+    const double vs = fmin(fabs(u), (double)SP_VMAX);
+    const double tt = fma(vs, (double)SP_SEG, shifter);
+    const uint32_t j = (uint32_t)orc_d2bits(tt);
+    const double kd = tt - shifter;
+    const double t = fma(-kd, 1.0 / SP_SEG, vs);
+    const double* c = orc_softplus_tab[j];
+    double p = c[9], d = c[9];
+    p = fma(p, t, c[8]);
+    for (int k = 7; k >= 0; --k) {
+        d = fma(d, t, p);
+        p = fma(p, t, c[k]);
+    }
+    *term = -(fmax(u, 0.0) + p);
+    const double sig = u >= 0.0 ? 1.0 + d : -d;
+    *rv = w * sig;
 }
 
 /* ------------------------------------------------------- Box-Muller angle */

@@ -255,6 +255,7 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
        order */
     const int rpw = geo.nw >= 4 ? 1 : 4 / geo.nw;
     double lik_part[8][4];
+    int logi_oos = 0;
     for (int s = 0; s < 8; ++s)
         for (int q = 0; q < 4; ++q) lik_part[s][q] = 0.0;
     for (int64_t i = 0; i < geo.n_pad; ++i) {
@@ -289,12 +290,14 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
                 const double A = (-(eta * eta + ORC_LOG2PI)) / 2.0;
                 r = y * orc_exp(A - la) - (1.0 - y) * orc_exp(A - lb);
             } else {
-                double tt = orc_exp_tab(-(sgn * eta));            /* prob = 1/(1+exp(-X*vars)) */
-                double p = 1.0 / (1.0 + tt);
-                term = orc_log_tab((y >= 0.5) ? p : 1.0 - p);     /* Y ~ Bernoulli(prob) */
-                /* d/deta of the Bernoulli term: the rule dd1 += 1/(p - 1 + y) (MCMCDerivRules.jl:111) times
-                   dprob/deta = s t / (1+t)^2 is s (y - p) for y in {0, 1}; the closed form is used */
-                r = sgn * (y - p);
+                /* prob = 1/(1+exp(-s X*vars)), Y ~ Bernoulli(prob): term = log(prob) or log(1 - prob), and d/deta
+                   of it, the rule dd1 += 1/(p - 1 + y) (MCMCDerivRules.jl:111) times dprob/deta = s t/(1+t)^2, which
+                   is s (y - p) for y in {0, 1}; both as functions of u = -w eta, w = s (2y - 1) (orc_logi) */
+                const double w = (y >= 0.5) ? sgn : -sgn;
+                orc_logi(eta, w, &term, &r);
+                /* -Inf where the reference's p rounds to 1 (y = 0) or 0 (y = 1): u = -w eta >= T(y) (glm_layout.hpp
+                   logi_bound: RU(53 ln 2); the first double past fdlibm exp's overflow threshold) */
+                if (-(w * eta) + ((y >= 0.5) ? -0x1.62e42fefa39f0p+9 : -0x1.25e4f7b2737fbp+5) >= 0.0) logi_oos = 1;
             }
             const int q = (int)(i & 3), rr = (int)((i & 15) >> 2);
             double* lp_ = lik_part[rr / rpw];
@@ -311,6 +314,7 @@ static double orc_glm_eval(const orc_model* m, const double* x, double* g, doubl
         const double w = (lik_part[s][0] + lik_part[s][2]) + (lik_part[s][1] + lik_part[s][3]);
         lik = s == 0 ? w : lik + w;
     }
+    if (logi_oos) lik = -INFINITY;
     for (int k = 0; k < dp; ++k) {
         double z = (xp[k] - 0.0) / sp;
         t[k] = -0.5 * (z * z + ORC_LOG2PI) - logsp;                /* vars ~ Normal(0, sp) */
@@ -923,6 +927,8 @@ void orc_detmath(int op, int64_t n, const double* x, const double* y, double* ou
             case 19: r = orc_log1p(a); break;
             case 20: r = orc_normlogcdf(a); break;
             case 21: r = orc_bm_radius_u32((uint32_t)(uint64_t)a); break;       /* device: the LDS-table path */
+            case 22: { double tm, rv; orc_logi(a, y[i], &tm, &rv); r = tm; break; }   /* logistic term (eta, w) */
+            case 23: { double tm, rv; orc_logi(a, y[i], &tm, &rv); r = rv; break; }   /* ... and its weight */
             case 8: {
                 uint32_t ctr[4] = {(uint32_t)(uint64_t)a, 0u, 0u, ORC_TAG_ACCEPT};
                 uint32_t key[2] = {0u, 0u}, w[4];

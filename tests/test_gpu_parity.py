@@ -57,7 +57,8 @@ def _dev_math(op, x, y=None):
                                      (11, "cos2pi_u32"), (12, "sqrt_pos_normal"), (13, "exp_tab"),
                                      (14, "log_tab"), (16, "bm_rad2_u32"),
                                      (17, "bm_radius_u32"), (18, "erfc"), (19, "log1p"),
-                                     (20, "normlogcdf"), (21, "bm_radius_u32_lds")])
+                                     (20, "normlogcdf"), (21, "bm_radius_u32_lds"), (22, "logi_term"),
+                                     (23, "logi_weight")])
 def test_device_detmath_bitwise(gpu, op, name):
     rng = np.random.default_rng(op)
     if op == 0:
@@ -101,9 +102,16 @@ def test_device_detmath_bitwise(gpu, op, name):
                             [0.0, 1.0, 5e-324, 2.2250738585072014e-308, np.nan]])
     elif op == 5:
         x = rng.normal(size=200000) * np.exp(rng.uniform(-300, 300, 200000))
+    elif op in (22, 23):         # eta over every table segment and both edges of each, beyond |u| = 40, specials
+        j = np.arange(0, 321) / 8.0
+        x = np.concatenate([rng.uniform(-45, 45, 200000), rng.normal(0, 3, 50000), rng.uniform(-800, 800, 5000),
+                            j + 1 / 16, j - 1 / 16, np.nextafter(j + 1 / 16, 0), -(j + 1 / 16), -(j - 1 / 16),
+                            [0.0, -0.0, 40.0, -40.0, 1e300, -1e300, np.inf, -np.inf]])
     else:
         x = np.concatenate([rng.uniform(-1e6, 1e6, 100000), np.arange(-50, 50) + 0.5])
     y = np.exp(rng.uniform(-300, 300, len(x))) if op == 5 else None
+    if op in (22, 23):           # w = s (2y - 1) in {-1, +1}
+        y = np.where(rng.random(len(x)) < 0.5, -1.0, 1.0)
     d, h = _dev_math(op, x, y), orc.detmath(op, x, y)
     same = (d.view(np.uint64) == h.view(np.uint64)) | (np.isnan(d) & np.isnan(h))
     assert same.all(), f"{name}: {np.count_nonzero(~same)} mismatches, e.g. x={x[~same][:3]}"

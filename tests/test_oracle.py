@@ -106,6 +106,44 @@ def test_log_tab_accuracy():
     sp = orc.detmath(14, np.array([0.0, 1.0, np.nan, 0.5]))
     assert sp[0] == -np.inf and sp[1] == 0.0 and np.isnan(sp[2]) and sp[3] == np.log(0.5)
 
+def test_logistic_term_accuracy():
+    """det_logi (round 5; the logistic Bernoulli term from one degree-9 segment polynomial and its derivative):
+    term = -softplus(u) and rv = w sigmoid(u), u = -w eta, against extended precision: the term within 2 ulp plus
+    2^-57 absolute (|u| > 40 holds f at f(40)), the weight within 3 ulp plus 2^-57 absolute, for both link signs
+    and both responses (w = s (2y - 1))."""
+    rng = np.random.default_rng(21)
+    eta = np.concatenate([rng.uniform(-45, 45, 200000), rng.normal(0, 3, 100000), rng.uniform(-800, 800, 20000),
+                          np.array([0.0, -0.0, 40.0, -40.0, 1e-300, 36.7368, 800.0])])
+    L = np.longdouble
+    for w in (1.0, -1.0):
+        ww = np.full_like(eta, w)
+        term, rv = orc.detmath(22, eta, ww), orc.detmath(23, eta, ww)
+        u = -(w * eta).astype(L)
+        sp = np.maximum(u, 0) + np.log1p(np.exp(-np.abs(u)))           # softplus(u)
+        sig = 1 / (1 + np.exp(-u))
+        t_ref, r_ref = (-sp).astype(float), (w * sig).astype(float)
+        assert (np.abs(term - t_ref) <= 2 * np.spacing(np.abs(t_ref)) + 2.0**-57).all()
+        assert (np.abs(rv - r_ref) <= 3 * np.spacing(np.abs(r_ref)) + 2.0**-57).all()
+    # at u = 0 both branches of the weight give exactly 1/2; the term is -log 2
+    assert orc.detmath(23, np.array([0.0, -0.0]), np.array([1.0, 1.0])).tolist() == [0.5, 0.5]
+    assert orc.detmath(22, np.array([0.0]), np.array([-1.0]))[0] == -np.log(2.0)
+
+
+@pytest.mark.parametrize("y", [0.0, 1.0])
+def test_logistic_reference_minus_inf_rule(y):
+    """The reference's p = 1/(1+exp(-X beta)) rounds to 1 (y = 0: log(1 - p) = -Inf) for X beta >= RU(53 ln 2) and
+    to 0 (y = 1: log(p) = -Inf) past exp's overflow threshold; the oracle's evaluation is -Inf (LLAcc: zero gradient)
+    from exactly those points on, and finite just before them."""
+    T = float.fromhex("0x1.25e4f7b2737fbp+5") if y == 0.0 else float.fromhex("0x1.62e42fefa39f0p+9")
+    sgn_eta = T if y == 0.0 else -T                         # u = -w eta = s eta (y = 0), -s eta (y = 1)
+    X = np.array([[1.0], [1.0]])
+    m = mc.model(mc.LogisticRegression(X, np.array([y, 1.0 - y]), prior_sigma=1e6), vars=np.zeros(1), gradient=True)
+    pts = np.array([[sgn_eta, np.nextafter(sgn_eta, 0.0)]])
+    lp, g = orc.eval_batch(m, pts)
+    assert lp[0] == -np.inf and g[0, 0] == 0.0
+    assert np.isfinite(lp[1]) and g[0, 1] != 0.0
+
+
 def test_det_sincos2pi_accuracy():
     rng = np.random.default_rng(2)
     u = np.floor(rng.uniform(0, 2**32, 100000)) * 2.0**-32
