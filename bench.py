@@ -622,7 +622,11 @@ def main():
         gbytes = sum(v.numel() * v.element_size() for v in gparts.values()) * world
         gather = {"gather_s": float(gmax[0]), "bytes": int(gbytes), "GB_per_s": gbytes / float(gmax[0]) / 1e9,
                   "kept_rows": rows, "of_kept_rows": nkept, "max_recv_buffer_bytes": gstats.get("max_recv_buffer_bytes"),
+                  "max_buffer_bytes_per_source": gstats.get("max_buffer_bytes_per_source"),
+                  "max_sources_in_flight": gstats.get("max_sources_in_flight"), "slots": gstats.get("slots"),
                   "note": "chunked point-to-point gather of the timed run's outputs into rank 0's host memory, "
+                          "receives from every source rank in flight together (two buffers per source), each "
+                          "landed chunk copied to page-locked host memory on a side stream while the next arrives; "
                           "timed apart (max over ranks); never inside the step loop"}
         del g_out, gparts
     spl = args.spl if args.spl >= 0 else 0

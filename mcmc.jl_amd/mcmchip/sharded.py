@@ -27,6 +27,7 @@ from .api import MCMCChain, MCMCTask, SerialMC, _unpack_bits
 __all__ = ["shard", "gather_shards", "run_sharded"]
 
 
+
 def shard(nchains: int, world: int, rank: int, align: int = 64):
     """(offset, count, block) of `rank`'s contiguous chain block; block = per-rank capacity (align multiple)."""
     if nchains <= 0 or world <= 0 or not 0 <= rank < world:
@@ -51,74 +52,159 @@ def _host_empty(shape, dtype, pin):
     return torch.empty(shape, dtype=dtype)
 
 
+class _Plan:
+    """The chunks of one array that one source rank sends to dst: (row0, nrows) runs of whole leading rows."""
+
+    def __init__(self, name, rows, width, woff, per):
+        self.name, self.rows, self.width, self.woff = name, rows, width, woff
+        self.chunks = [(r0, min(per, rows - r0)) for r0 in range(0, rows, per)]
+
+
 def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None, dst: int = 0,
-                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, stats: Optional[dict] = None):
+                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, stats: Optional[dict] = None, slots: int = 2):
     """Gather per-rank arrays whose LAST axis is the rank's chain block into host memory on `dst`.
 
     parts: name -> torch tensor [..., count] (accept bits: [..., ceil(count/64)] words), on the rank's GPU
     (NCCL) or on the host (gloo).  Rank r's columns are the global chains shard(nchains, world, r).  The
-    transfer is point to point, rank by rank and chunk by chunk: a chunk is a run of whole leading rows
-    (e.g. kept steps) of at most `chunk_bytes`, sent by its rank and received on `dst` into ONE reused
-    buffer, then copied straight into the destination's host array.  So `dst` never holds more than one
-    chunk of another rank's data on its device (the world's outputs are never concatenated on one GPU:
-    at the 8-GPU metric they would be 193 GB).  Returns name -> numpy array over all `nchains` chains
-    (bits: ceil(nchains/64) words) on dst, None elsewhere.  `stats` (a dict, dst only) receives
-    `max_recv_buffer_bytes` and `bytes` (bytes received from other ranks)."""
+    transfer is point to point in chunks (runs of whole leading rows, e.g. kept steps, of at most `chunk_bytes`)
+    and concurrent across sources: dst keeps up to `slots` receives in flight from EVERY source rank at once, each
+    into its own buffer, and as a receive lands its chunk goes on to host memory (NCCL: an asynchronous device ->
+    page-locked host copy on a side stream, so the next receive into the other buffer overlaps it) and is then
+    placed into the destination array.  So `dst` holds at most `slots` chunks per source on its device (the world's
+    outputs are never concatenated on one GPU: at the 8-GPU metric they would be 193 GB).  Returns name -> numpy
+    array over all `nchains` chains (bits: ceil(nchains/64) words) on dst, None elsewhere.  `stats` (a dict, dst
+    only) receives `bytes` (received from other ranks), `max_recv_buffer_bytes` (the largest one buffer),
+    `max_buffer_bytes_per_source`, `max_sources_in_flight` (source ranks with a receive outstanding at one time)
+    and `max_chunks_in_flight`."""
+    import collections
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if chunk_bytes <= 0:
         raise ValueError("chunk_bytes must be > 0")
+    if slots < 1:
+        raise ValueError("slots must be >= 1")
     on_gpu = dist.get_backend(group) == "nccl"
-    out = {} if rank == dst else None
-    max_buf = 0
-    moved = 0
-    for name, t in parts.items():
-        is_bits = name == "accept_bits"
-        lead = tuple(t.shape[:-1])
-        rows = 1
-        for n in lead:
-            rows *= n
-        esize = t.element_size()
-        keep = (nchains + 63) // 64 if is_bits else nchains
-        host = None
-        if rank == dst:
-            host = _host_empty((rows, keep), t.dtype, on_gpu and torch.cuda.is_available())
-        buf = None
-        for r in range(world):
-            off, cnt, _ = shard(nchains, world, r)
-            if cnt <= 0:
-                continue
-            woff = off // 64 if is_bits else off
+    glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    names = list(parts)
+    # per array: its host destination (dst) and each rank's plan
+    lead = {n: tuple(parts[n].shape[:-1]) for n in names}
+    rowsof = {n: int(np.prod(lead[n], dtype=np.int64)) if lead[n] else 1 for n in names}
+    plans = {}                                            # source rank -> [_Plan] in send order
+    for r in range(world):
+        off, cnt, _ = shard(nchains, world, r)
+        plans[r] = []
+        if cnt <= 0:
+            continue
+        for n in names:
+            is_bits = n == "accept_bits"
             width = (cnt + 63) // 64 if is_bits else cnt
-            per = max(1, chunk_bytes // max(1, width * esize))
-            if r == rank:
-                mine = t.reshape(rows, t.shape[-1])[:, :width]
-                if rank == dst:
-                    host[:, woff:woff + width].copy_(mine)
-                else:
-                    for r0 in range(0, rows, per):
-                        dist.send(mine[r0:r0 + per].contiguous(), dst=dist.get_global_rank(group, dst)
-                                  if group is not None else dst, group=group)
-            elif rank == dst:
-                src = dist.get_global_rank(group, r) if group is not None else r
-                for r0 in range(0, rows, per):
-                    n = min(per, rows - r0)
-                    need = n * width
-                    if buf is None or buf.numel() < need:
-                        buf = torch.empty(max(need, min(rows, per) * width), dtype=t.dtype, device=t.device)
-                        max_buf = max(max_buf, buf.numel() * esize)
-                    view = buf[:need].view(n, width)
-                    dist.recv(view, src=src, group=group)
-                    host[r0:r0 + n, woff:woff + width].copy_(view)
-                    moved += need * esize
-        buf = None
-        if rank == dst:
-            out[name] = host.numpy().reshape(lead + (keep,))
-    if stats is not None and rank == dst:
-        stats["max_recv_buffer_bytes"] = max_buf
-        stats["bytes"] = moved
+            per = max(1, chunk_bytes // max(1, width * parts[n].element_size()))
+            plans[r].append(_Plan(n, rowsof[n], width, off // 64 if is_bits else off, per))
+    out = None
+    if rank != dst:
+        # the sender: every chunk of every array in plan order, at most `slots` sends outstanding
+        works = collections.deque()
+        for pl in plans[rank]:
+            mine = parts[pl.name].reshape(pl.rows, parts[pl.name].shape[-1])[:, :pl.width]
+            for r0, n in pl.chunks:
+                while len(works) >= slots:
+                    works.popleft().wait()
+                works.append(dist.isend(mine[r0:r0 + n].contiguous(), dst=glob(dst), group=group))
+        while works:
+            works.popleft().wait()
+        return None
+    # dst: host arrays, its own columns copied directly
+    host = {}
+    for n in names:
+        is_bits = n == "accept_bits"
+        keep = (nchains + 63) // 64 if is_bits else nchains
+        host[n] = _host_empty((rowsof[n], keep), parts[n].dtype, False).numpy()
+    for pl in plans[dst]:
+        mine = parts[pl.name].reshape(pl.rows, parts[pl.name].shape[-1])[:, :pl.width]
+        host[pl.name][:, pl.woff:pl.woff + pl.width] = mine.cpu().numpy()
+    queues = {r: collections.deque((pl, r0, n) for pl in plans[r] for r0, n in pl.chunks)
+              for r in range(world) if r != dst and plans[r]}
+    dev = next(iter(parts.values())).device
+    esz = {n: parts[n].element_size() for n in names}
+    dtype = {n: parts[n].dtype for n in names}
+    side = torch.cuda.Stream(device=dev) if on_gpu else None
+    bufs = {}                                             # (source, slot) -> device (or host) buffer, reused
+    stage = {}                                            # (source, slot) -> page-locked host staging (NCCL)
+    free = {r: collections.deque(range(slots)) for r in queues}
+    flight = collections.deque()                          # (source, slot, plan, row0, nrows, work) in post order
+    copying = collections.deque()                         # (source, slot, plan, row0, nrows, event): D2H under way
+    max_buf = max_src_buf = moved = 0
+    max_src = max_chunks = 0
+    src_buf_bytes = collections.Counter()
+
+    def buffer(key, pl, n):
+        need = n * pl.width * esz[pl.name]
+        b = bufs.get(key)
+        if b is None or b.numel() * b.element_size() < need:
+            nonlocal max_buf, max_src_buf
+            old = 0 if b is None else b.numel() * b.element_size()
+            b = torch.empty(need, dtype=torch.uint8, device=dev)
+            bufs[key] = b
+            src_buf_bytes[key[0]] += need - old
+            max_buf = max(max_buf, need)
+            max_src_buf = max(max_src_buf, src_buf_bytes[key[0]])
+            if on_gpu:
+                stage[key] = _host_empty((need,), torch.uint8, True)
+        return b[:need].view(dtype[pl.name]).view(n, pl.width)
+
+    def place(pl, r0, n, arr):
+        host[pl.name][r0:r0 + n, pl.woff:pl.woff + pl.width] = arr
+
+    def finish_copies(block_all):
+        while copying and (block_all or copying[0][5].query()):
+            r, k, pl, r0, n, ev = copying.popleft()
+            ev.synchronize()
+            st = stage[(r, k)][:n * pl.width * esz[pl.name]].view(dtype[pl.name]).view(n, pl.width)
+            place(pl, r0, n, st.numpy())
+            free[r].append(k)
+
+    t0 = time.perf_counter()
+    while queues or flight or copying:
+        # post: every source with a chunk left and a free buffer
+        for r in list(queues):
+            while queues[r] and free[r]:
+                pl, r0, n = queues[r].popleft()
+                k = free[r].popleft()
+                view = buffer((r, k), pl, n)
+                flight.append((r, k, pl, r0, n, view, dist.irecv(view, src=glob(r), group=group)))
+            if not queues[r]:
+                del queues[r]
+        max_chunks = max(max_chunks, len(flight))
+        max_src = max(max_src, len({f[0] for f in flight}))
+        if flight:
+            r, k, pl, r0, n, view, work = flight.popleft()
+            work.wait()
+            moved += n * pl.width * esz[pl.name]
+            if on_gpu:
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    st = stage[(r, k)][:n * pl.width * esz[pl.name]].view(dtype[pl.name]).view(n, pl.width)
+                    st.copy_(view, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                # the next receive into this buffer runs on the NCCL stream after the current stream: make the
+                # current stream wait for the copy out of it
+                torch.cuda.current_stream(dev).wait_event(ev)
+                copying.append((r, k, pl, r0, n, ev))
+                finish_copies(False)
+            else:
+                place(pl, r0, n, view.numpy())
+                free[r].append(k)
+        else:
+            finish_copies(True)
+    out = {n: host[n].reshape(lead[n] + (host[n].shape[1],)) for n in names}
+    if stats is not None:
+        sec = time.perf_counter() - t0
+        stats.update(bytes=moved, max_recv_buffer_bytes=max_buf, max_buffer_bytes_per_source=max_src_buf,
+                     max_sources_in_flight=max_src, max_chunks_in_flight=max_chunks, slots=slots, seconds=sec,
+                     GB_per_s=moved / sec / 1e9 if sec > 0 else None)
     return out
 
 

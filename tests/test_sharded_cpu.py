@@ -52,7 +52,7 @@ def _fake_shard(off, cnt, nk, d):
     return samples, acc, words
 
 
-def _worker(rank, world, port, total, nk, d, q, chunk=None):
+def _worker(rank, world, port, total, nk, d, q, chunk=None, slots=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -61,7 +61,7 @@ def _worker(rank, world, port, total, nk, d, q, chunk=None):
         parts = {"samples": torch.from_numpy(s), "accept_bits": torch.from_numpy(words.view(np.int64)),
                  "final_lp": torch.from_numpy(s[-1, 0].copy())}
         stats = {}
-        kw = {} if chunk is None else {"chunk_bytes": chunk}
+        kw = {"slots": slots} if chunk is None else {"chunk_bytes": chunk, "slots": slots}
         full = gather_shards(parts, cnt, block, total, dst=0, stats=stats, **kw)
         if rank == 0:
             res = {k: v.copy() for k, v in full.items()}
@@ -73,12 +73,13 @@ def _worker(rank, world, port, total, nk, d, q, chunk=None):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("total,chunk", [(130, None), (1000, None), (1000, 8 * 500 * 2), (777, 64)])
-def test_gather_shards_gloo_world2(total, chunk):
+@pytest.mark.parametrize("world,total,chunk", [(2, 130, None), (2, 1000, None), (2, 1000, 8 * 500 * 2), (2, 777, 64),
+                                               (3, 1000, 8 * 300), (3, 5000, 8 * 1000), (4, 3000, 64)])
+def test_gather_shards_gloo(world, total, chunk):
     """The chunked point-to-point gather reassembles every array exactly, whatever the chunk size (64 B: one
-    row per message), and the destination's receive buffer never exceeds one chunk (one row when a row is
-    larger than the chunk)."""
-    nk, d, world = 3, 2, 2
+    row per message); every receive buffer holds at most one chunk (one row when a row is larger than the chunk),
+    at most two per source rank, and with several source ranks their receives are in flight together."""
+    nk, d = 3, 2
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -96,7 +97,12 @@ def test_gather_shards_gloo_world2(total, chunk):
     assert np.array_equal(full["final_lp"], s[-1, 0])
     assert np.array_equal(full["accept_bits"].view(np.uint64), words)
     st = full["_stats"]
-    _, cnt1, _ = shard(total, world, 1)
-    assert st["bytes"] == 8 * cnt1 * (nk * d + 1) + 8 * nk * ((cnt1 + 63) // 64)
+    cnts = [shard(total, world, r)[1] for r in range(1, world)]
+    assert st["bytes"] == sum(8 * c * (nk * d + 1) + 8 * nk * ((c + 63) // 64) for c in cnts)
+    one = max(8 * c for c in cnts)                         # the largest row of any array
     if chunk is not None:
-        assert st["max_recv_buffer_bytes"] <= max(chunk, 8 * cnt1)
+        assert st["max_recv_buffer_bytes"] <= max(chunk, one)
+        assert st["max_buffer_bytes_per_source"] <= 2 * max(chunk, one)
+    if sum(c > 0 for c in cnts) >= 2:
+        assert st["max_sources_in_flight"] >= 2             # receives from several ranks outstanding together
+    assert st["GB_per_s"] > 0
