@@ -58,6 +58,14 @@ CONFIGS = {
                            "the configured burnin (100 steps of dual averaging, HMCDA.jl:133-138) runs untimed as the "
                            "warmup, then the timed steps run at each chain's adapted dualLeapStep: a step is "
                            "round(len/eps) leapfrogs of that chain (HMCDA.jl:104)"),
+    # round 5: the widened regression sizes (not BASELINE configs)
+    "linear1024": dict(model="linear", d=1024, n=4096, chains=65536 // 8, sampler="hmcda", steps=10, warmup=100,
+                       thinning=1, adapt=True,
+                       desc="linear regression n=4096 d=1024 (config 5 at twice its width: eight 128-coordinate "
+                            "slices a chain tile), HMCDA(), 8,192 chains, adapted as linear512"),
+    "ramlinear128": dict(model="linear", d=128, n=1000, chains=1 << 15, sampler="ram", steps=40, warmup=10,
+                         thinning=10, desc="RAM(1., 0.3) on linear regression n=1000 d=128, 32,768 chains (the "
+                                           "split step: regression eval kernel + wave-per-chain factor update)"),
     # the reference's own published benchmark unit (benchmarks/benchunits/binomial.jl:1-25, benchlog.csv:350-352)
     "binomial": dict(model="logistic", d=10, n=1000, chains=1 << 18, sampler="rwm", steps=100, warmup=10,
                      thinning=1, desc="benchmarks/benchunits/binomial.jl: logistic regression n=1000 d=10, "

@@ -181,7 +181,7 @@ int mcmc_runner_validate(const mcmc_runner_cfg* cfg);
  * stream is keyed by (seed, global chain, global step), so results do not
  * depend on the number of GPUs.  init_x: optional per-chain start [d][nchains]
  * (NULL -> every chain starts at model.init, RWM.jl:53).  Sizes built: d <= 16384 for the separable
- * models, d <= 1024 for the regression models; RAM d <= 1024 (separable) / d <= 32 (regression), else
+ * models, d <= 1024 for the regression models; RAM d <= 1024 (separable and regression), else
  * MCMC_E_UNSUPPORTED. */
 int mcmc_chains_create(mcmc_model* model, const mcmc_sampler_cfg* sampler, int64_t nchains,
                        int64_t chain_offset, uint64_t seed, const double* init_x, mcmc_chains** out);

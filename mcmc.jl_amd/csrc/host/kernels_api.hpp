@@ -40,6 +40,11 @@ hipError_t mcmc_launch_glm_record(const mcmc::KernelArgs& a, const mcmc::LeapRec
 hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, double* lp, double* g, int check,
                                 hipStream_t st);
 int mcmc_glm_max_d();
+// RAM on regression targets, 32 < d <= 1024 (glm_ram_wave.hip): per step the eval kernel and the accept / factor-update
+// kernel; u [C][ustride], nz [C], xprop [d][ld], lpp [C] are the device buffers between them
+hipError_t mcmc_launch_glm_ram_wave(const mcmc::KernelArgs& a, double* u, double* nz, double* xprop, double* lpp,
+                                    hipStream_t st);
+int64_t mcmc_glm_ram_wave_ustride(int d);
 // SeqMC population bookkeeping (seqmc.hip)
 hipError_t mcmc_seqmc_weights(int64_t N, double* logW, const double* ll0, double* logtarget, const double* plogtarget,
                               hipStream_t st);

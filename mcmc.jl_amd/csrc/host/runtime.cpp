@@ -101,6 +101,9 @@ struct mcmc_chains {
     double* d_scale_eff = nullptr;   // model.scale .* sampler.scale (RWM.jl:52)
     std::vector<double> h_scale_eff; // its host copy
     int ram_dpad = 0;                // RAM: padded factor width
+    bool ram_wave = false;           // RAM: the factor in the wave-per-chain layout (separable d > 32, regression d > 32)
+    bool glm_ram_wave = false;       // RAM on a regression target with d > 32: the split step (glm_ram_wave.hip)
+    double *ram_u = nullptr, *ram_nz = nullptr, *xprop = nullptr, *lpp = nullptr;   // ... its buffers
     double scale1 = 0.0;             // its common value when all coordinates agree
     int32_t scale_uniform = 0;
     double* d_init_x = nullptr;      // optional per-chain start, [d][C]
@@ -593,6 +596,12 @@ static void free_state(mcmc_chains* c) {
     s = ChainState{};
 }
 
+// the step kernels of one launch; RAM on a regression target with d > 32 is a sequence of kernels per step
+static hipError_t launch_chain_step(const mcmc_chains* c, const KernelArgs& a, hipStream_t st) {
+    if (c->glm_ram_wave) return mcmc_launch_glm_ram_wave(a, c->ram_u, c->ram_nz, c->xprop, c->lpp, st);
+    return launch_step(c->layout, a, st);
+}
+
 // RWM, MALA and RAM evaluate the log-target once per chain-step, so a launch of n steps adds C n evaluations:
 // counted on the host.  The step kernels count only where the count is data-dependent (HMC / HMCDA trajectories):
 // one device-scope atomic per wave on a single address serialises at the memory side (32 768 of them per 2^20-chain
@@ -668,7 +677,7 @@ static int init_state(mcmc_chains* c) {
         // (ram.hpp), diagonal (r, r) at row r(r+1)/2 + r of every tile; the padding block d..dpad-1 is the identity
         const int64_t rl = c->st.ram_ld;
         HIP_TRY(hipMemsetAsync(c->st.ram_L, 0, 2 * (size_t)c->st.ram_hs * 8, st));
-        if (c->layout == LAYOUT_WPC) {                     // diagonal (k, k) at colstart(k) of every chain block
+        if (c->ram_wave) {                                 // diagonal (k, k) at colstart(k) of every chain block
             for (int k = 0; k < d; ++k)
                 HIP_TRY(mcmc_fill_f64_strided(c->st.ram_L + wave_colstart(k, d), c->st.ram_hs / rl, 1, rl,
                                               c->h_scale_eff[k], st));
@@ -699,9 +708,6 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     if (nchains <= 0) return fail(MCMC_E_INVALID_ARG, "nchains should be > 0");
     if (chain_offset < 0 || chain_offset + nchains > (int64_t)0x100000000LL)
         return fail(MCMC_E_INVALID_ARG, "global chain ids must fit in 32 bits");
-    if (s->kind == MCMC_RAM && !model_is_separable(m) && m->args.d > 32)
-        return fail(MCMC_E_UNSUPPORTED, "RAM on regression targets is built for d <= 32 (the d x d jump factor of every "
-                                        "chain is kept in HBM)");
     if (s->kind == MCMC_RAM && m->args.d > mcmc_wpc_ram_max_d())
         return fail(MCMC_E_UNSUPPORTED, "RAM is built for d <= " + std::to_string(mcmc_wpc_ram_max_d()) +
                                         " (the d x d jump factor of every chain is kept in HBM)");
@@ -772,7 +778,9 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
     c->h_scale_eff = se;
     if (sa.kind == SK_RAM) {
         // padded width: the lane-per-chain kernel's NC = 4 ceil(d/4), the regression kernel's DF = d_pad
-        if (c->layout == LAYOUT_WPC) {
+        c->ram_wave = c->layout == LAYOUT_WPC || (c->layout == LAYOUT_GLM && d > 32);
+        c->glm_ram_wave = c->layout == LAYOUT_GLM && d > 32;
+        if (c->ram_wave) {
             // wave-per-chain: [half][chain][column-major packed factor] (ram.hpp wave layout), one block per chain of
             // every launched wave (8 chains per workgroup when two chains share a wave)
             c->ram_dpad = d;
@@ -784,6 +792,12 @@ extern "C" int mcmc_chains_create(mcmc_model* m, const mcmc_sampler_cfg* s, int6
             c->st.ram_hs = (int64_t)(ram_nrows(c->ram_dpad) + 1) * c->st.ram_ld;
         }
         if (int r = dmalloc(&c->st.ram_L, 2 * (size_t)c->st.ram_hs)) return bail(r);
+        if (c->glm_ram_wave) {
+            if (int r = dmalloc(&c->ram_u, (size_t)nchains * (size_t)mcmc_glm_ram_wave_ustride(d))) return bail(r);
+            if (int r = dmalloc(&c->ram_nz, (size_t)nchains)) return bail(r);
+            if (int r = dmalloc(&c->xprop, nst)) return bail(r);
+            if (int r = dmalloc(&c->lpp, nc)) return bail(r);
+        }
     }
     c->scale1 = se.empty() ? 0.0 : se[0];
     c->scale_uniform = 1;
@@ -819,6 +833,10 @@ extern "C" int mcmc_chains_destroy(mcmc_chains* c) {
     dfree(c->out_tmp.p);
     dfree(c->stage_samples.p);
     dfree(c->stage_grads.p);
+    dfree(c->ram_u);
+    dfree(c->ram_nz);
+    dfree(c->xprop);
+    dfree(c->lpp);
     mcmc_model* m = c->model;
     delete c;
     if (--m->chains_alive == 0 && m->released) model_free(m);
@@ -920,7 +938,7 @@ extern "C" int mcmc_chains_fork(mcmc_chains* src, int64_t first, int64_t count, 
         const size_t half = (size_t)(src->steps_done & 1);
         const double* sh = src->st.ram_L + half * (size_t)src->st.ram_hs;
         double* dh = c->st.ram_L + half * (size_t)c->st.ram_hs;
-        if (c->layout == LAYOUT_WPC) {                     // [chain][ram_ld]
+        if (c->ram_wave) {                                 // [chain][ram_ld]
             e = hipMemcpyAsync(dh, sh + (size_t)first * src->st.ram_ld, (size_t)count * c->st.ram_ld * 8,
                                hipMemcpyDeviceToDevice, st);
         } else {                                           // [64-chain tile][row][64]: re-tile on the host
@@ -974,7 +992,7 @@ extern "C" int mcmc_chains_ram_factor(mcmc_chains* c, double* S) {
     const size_t rows = ram_nrows(c->model->args.d);          // the leading rows of the padded packing
     const size_t rl = (size_t)c->st.ram_ld;
     const double* cur = c->st.ram_L + (size_t)(c->steps_done & 1) * (size_t)c->st.ram_hs;   // written last
-    if (c->layout == LAYOUT_WPC) {                             // [chain][column-major packed] -> [row][chain]
+    if (c->ram_wave) {                                         // [chain][column-major packed] -> [row][chain]
         const int64_t d = c->model->args.d;
         std::vector<double> h((size_t)c->C * rl);
         HIP_TRY(hipMemcpyAsync(h.data(), cur, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1260,7 +1278,7 @@ int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs*
             HIP_TRY(launch_record(L, a, lr, st));
         }
         g_step_kernel[0] = 0;
-        HIP_TRY(launch_step(L, a, st));
+        HIP_TRY(launch_chain_step(c, a, st));
         c->step_kernel = g_step_kernel;
         if (host_evals) c->h_evals += C * n;
     }
@@ -1357,7 +1375,7 @@ static int step_once(mcmc_chains* c, hipStream_t st) {
     s.n_evals = evals_on_host(c) ? nullptr : c->d_evals;
     s.step_begin = c->steps_done + 1;
     s.nsteps = 1;
-    HIP_TRY(launch_step(c->layout, a, st));
+    HIP_TRY(launch_chain_step(c, a, st));
     if (evals_on_host(c)) c->h_evals += c->C;
     c->steps_done += 1;
     return MCMC_OK;

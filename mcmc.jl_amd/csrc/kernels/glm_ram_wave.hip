@@ -1,0 +1,204 @@
+// glm_ram_wave.hip -- robust adaptive Metropolis (src/samplers/RAM.jl:41-79) on the regression targets for
+// 32 < d <= 1024.  The d x d jump factor of a chain is as large as the rows of X a 16-chain MFMA tile streams per
+// evaluation, so the step is split across three kernels instead of fused into glm_ram's tile loop:
+//   glm_ram_prop    (once per launch sequence)  rvec = randn(d), u = S rvec, |rvec|^2; xprop = x + u      (RAM.jl:58-60)
+//   glm eval kernel (every step)                lpp = log-target at xprop (the regression MFMA evaluation)
+//   glm_ram_update  (every step)                the MH test (RAM.jl:62-71), the factor update (RAM.jl:74-78) with
+//                                               the next step's S rvec folded into it (ram_wave_update NEXT), and
+//                                               the next xprop
+// The factor is the wave-per-chain layout of ram_wave.hpp (one chain per wave, its rows over the 64 lanes); x stays
+// in the regression layout [d][ld] (the eval kernel's input), read and written per coordinate.  u (row layout) and
+// |rvec|^2 wait in HBM between the kernels.  Sums: the matvec and the update are ram_wave.hpp's, |rvec|^2 the
+// 64-lane wave order; oracle.c restates both (orc_chain, RAM on a regression target with d > 32).
+#include "wpc_impl.hpp"
+#include "../ram_wave.hpp"
+
+namespace mcmc {
+
+// WaveChain's coordinate layout (lane l, slot 4 g + e <-> coordinate 4 (l + 64 g) + e) over the regression state
+// [d][ld] and the C ABI's kept layout [nkept][d][C]
+template <int G>
+struct GlmWaveChain : WaveChain<G, false, 1, kTabGlobal> {
+    using Base = WaveChain<G, false, 1, kTabGlobal>;
+    using Base::c;
+    using Base::coord;
+    using Base::live;
+    using Base::valid;
+    static constexpr int NC = Base::NC;
+    int64_t ld;
+    __device__ explicit GlmWaveChain(const StepArgs& s) : Base(s) { ld = s.ld; }
+    __device__ __forceinline__ void load_glm(const double* x, double (&v)[NC]) const {
+        const int64_t cc = live ? c : 0;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) v[k] = valid(k) ? x[(size_t)coord(k) * (size_t)ld + (size_t)cc] : 0.0;
+    }
+    __device__ __forceinline__ void store_glm(double* x, const double (&v)[NC]) const {
+        if (!live) return;
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (valid(k)) x[(size_t)coord(k) * (size_t)ld + (size_t)c] = v[k];
+    }
+    __device__ __forceinline__ void store_kept_glm(const StepArgs& s, int64_t kk, const double (&v)[NC]) const {
+        if (s.samples == nullptr || !live) return;
+        double* p = s.samples + (size_t)kk * (size_t)s.d * (size_t)s.C + (size_t)c;
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+            if (valid(k)) p[(size_t)coord(k) * (size_t)s.C] = v[k];
+    }
+};
+
+// the per-chain buffers between the kernels: u = S rvec in row layout [C][64 NC] and |rvec|^2 [C]
+struct GlmRamBufs {
+    double* u;
+    double* nz;
+    double* xprop;      // [d][ld]
+    const double* lpp;  // [C]
+};
+
+template <int G>
+__device__ __forceinline__ uint32_t glm_ram_vo(const GlmWaveChain<G>& p) { return (uint32_t)p.lane * 8u; }
+
+// rvec of step i, |rvec|^2 (wave order), u = S_(i-1) rvec; xprop = x + u
+template <int G>
+__global__ __launch_bounds__(kBlock) void glm_ram_prop(KernelArgs a, GlmRamBufs b) {
+    using P = GlmWaveChain<G>;
+    constexpr int NC = P::NC, L = 64;
+    const StepArgs& s = a.s;
+    const P p(s);
+    if (!p.live) return;                                          // wave-uniform: one chain a wave
+    __shared__ double xpose[kBlock / 64][64 * NC];
+    double* const slice = xpose[threadIdx.x >> 6];
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int d = s.d;
+    const int64_t i = s.step_begin;
+    double z[NC], zr[NC], u[NC], uq[NC], x[NC];
+    gen_normals(p, rs, chain, (uint32_t)i, z);                    // rvec = randn(d)
+    double a2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        if (!p.valid(k)) z[k] = 0.0;
+        a2 = __builtin_fma(z[k], z[k], a2);                       // dot(rvec, rvec)
+    }
+    const double nz = p.reduce(a2);
+    ram_to_rows<NC, L>(slice, p.lane, z, zr);
+    const int64_t ld = a.st.ram_ld;
+    double* const B0 = a.st.ram_L + (uint64_t)p.c * (uint64_t)ld;
+    const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * (uint64_t)a.st.ram_hs, ld * 8);
+    ram_wave_matvec<NC, L>(Ss, glm_ram_vo(p), p.lane, d, zr, u);  // S * rvec
+#pragma unroll
+    for (int sl = 0; sl < NC; ++sl) b.u[(size_t)p.c * (64 * NC) + (size_t)(p.lane + L * sl)] = u[sl];
+    if (p.lane == 0) b.nz[p.c] = nz;
+    ram_to_quads<NC, L>(slice, p.lane, u, uq);
+    p.load_glm(a.st.x, x);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) x[k] = x[k] + uq[k];             // RAM.jl:60
+    p.store_glm(b.xprop, x);
+}
+
+// step i: accept (RAM.jl:62-71), kept rows, the factor update (RAM.jl:74-78); NEXT: step i + 1's u, |rvec|^2, xprop
+template <int G, bool NEXT>
+__global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBufs b) {
+    using P = GlmWaveChain<G>;
+    constexpr int NC = P::NC, L = 64;
+    const StepArgs& s = a.s;
+    const SamplerArgs& sa = a.sa;
+    const P p(s);
+    if (!p.live) return;
+    __shared__ double xpose[kBlock / 64][64 * NC];
+    double* const slice = xpose[threadIdx.x >> 6];
+    const Stream rs{s.key0, s.key1};
+    const uint32_t chain = s.chain0 + (uint32_t)p.c;
+    const int d = s.d;
+    const int64_t i = s.step_begin;
+    double x[NC], u[NC], uq[NC];
+    p.load_glm(a.st.x, x);
+    double lp = a.st.lp[p.c];
+    const double lpp = b.lpp[p.c];
+#pragma unroll
+    for (int sl = 0; sl < NC; ++sl) u[sl] = b.u[(size_t)p.c * (64 * NC) + (size_t)(p.lane + L * sl)];
+    const double nz = b.nz[p.c];
+    ram_to_quads<NC, L>(slice, p.lane, u, uq);
+    const double ratio = lpp - lp;
+    const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
+    if (acc) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) x[k] = x[k] + uq[k];         // the proposal xprop, the same sums
+        lp = lpp;
+    }
+    Keeper keep(s);
+    int64_t kk;
+    if (keep.take(i, &kk)) {
+        p.store_kept_glm(s, kk, x);
+        p.store_bit(s, kk, acc);
+    }
+    const double alpha = ram_alpha(i, d, ratio, sa.rate);
+    const int64_t ld = a.st.ram_ld;
+    double* const B0 = a.st.ram_L + (uint64_t)p.c * (uint64_t)ld;
+    const uint64_t hs = (uint64_t)a.st.ram_hs;
+    const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld * 8);
+    const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, ld * 8);
+    double zn[NC], znr[NC], un[NC];
+    double a2 = 0.0;
+    if (NEXT) {
+        gen_normals(p, rs, chain, (uint32_t)(i + 1), zn);          // step i + 1's rvec
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            if (!p.valid(k)) zn[k] = 0.0;
+            a2 = __builtin_fma(zn[k], zn[k], a2);
+        }
+        ram_to_rows<NC, L>(slice, p.lane, zn, znr);
+    }
+    ram_wave_update<NC, L, NEXT>(Ss, Sd, glm_ram_vo(p), p.lane, d, alpha, nz, u, znr, un);
+    p.store_glm(a.st.x, x);
+    if (p.lane == 0) a.st.lp[p.c] = lp;
+    if (NEXT) {
+#pragma unroll
+        for (int sl = 0; sl < NC; ++sl) b.u[(size_t)p.c * (64 * NC) + (size_t)(p.lane + L * sl)] = un[sl];
+        const double nzn = p.reduce(a2);
+        if (p.lane == 0) b.nz[p.c] = nzn;
+        ram_to_quads<NC, L>(slice, p.lane, un, uq);
+#pragma unroll
+        for (int k = 0; k < NC; ++k) x[k] = x[k] + uq[k];
+        p.store_glm(b.xprop, x);
+    }
+}
+
+template <int G>
+static hipError_t glm_ram_wave_g(const KernelArgs& a0, const GlmRamBufs& b0, double* lpp, hipStream_t st) {
+    const dim3 grid((unsigned)((a0.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    KernelArgs a = a0;
+    GlmRamBufs b = b0;
+    b.lpp = lpp;
+    a.s.nsteps = 1;
+    glm_ram_prop<G><<<grid, kBlock, 0, st>>>(a, b);
+    hipError_t e = hipGetLastError();
+    for (int t = 0; t < a0.s.nsteps && e == hipSuccess; ++t) {
+        a.s.step_begin = a0.s.step_begin + t;
+        e = mcmc_launch_glm_eval(a, b.xprop, lpp, nullptr, 0, st);           // the log-target at xprop
+        if (e != hipSuccess) break;
+        if (t + 1 < a0.s.nsteps) glm_ram_update<G, true><<<grid, kBlock, 0, st>>>(a, b);
+        else glm_ram_update<G, false><<<grid, kBlock, 0, st>>>(a, b);
+        e = hipGetLastError();
+    }
+    return e;
+}
+
+}  // namespace mcmc
+
+// doubles of the row-layout u buffer per chain (64 NC)
+int64_t mcmc_glm_ram_wave_ustride(int d) { return d <= 256 ? 256 : d <= 512 ? 512 : 1024; }
+
+hipError_t mcmc_launch_glm_ram_wave(const mcmc::KernelArgs& a, double* u, double* nz, double* xprop, double* lpp,
+                                    hipStream_t st) {
+    using namespace mcmc;
+    const GlmRamBufs b{u, nz, xprop, nullptr};
+    const int g = wpc_nb_for(a.s.d);
+    mcmc_note_step_kernel("glm_ram_update<%d, true>", g);
+    switch (g) {
+        case 1: return glm_ram_wave_g<1>(a, b, lpp, st);
+        case 2: return glm_ram_wave_g<2>(a, b, lpp, st);
+        case 4: return glm_ram_wave_g<4>(a, b, lpp, st);
+        default: return hipErrorInvalidValue;
+    }
+}

@@ -119,12 +119,20 @@ static int orc_is_glm(const orc_model* m) {
    coordinates left to right, the rest left to right, then (first) + (second) */
 static int orc_pair_split(int d) { return 4 * (((d + 3) / 4 + 1) / 2); }
 
+static double orc_dot_lanes(const double* v, int d, int order);
+
 static double orc_dot(const double* v, const orc_model* mdl, int order) {
     const int d = mdl->d;
     if (orc_is_glm(mdl)) {
         orc_glm_geo geo = orc_glm_geometry(mdl);
         return orc_glm_sum(v, &geo, d, 1);
     }
+    return orc_dot_lanes(v, d, order);
+}
+
+/* v . v in a kernel family's order: 0 left to right, ORC_ORDER_PAIR, ORC_ORDER_HALF, or W = order
+   waves of 64 lanes (lane partials, then the butterfly, waves left to right) */
+static double orc_dot_lanes(const double* v, int d, int order) {
     if (order == ORC_ORDER_PAIR) {
         const int S = orc_pair_split(d);
         double a = 0.0, b = 0.0;
@@ -659,9 +667,11 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
             double* Lc = st->ram_L + c;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* rvec = randn(d) */
             double nz = 0.0;                                                  /* dot(rvec, rvec): in order, */
-            if (order == 0 || order == ORC_ORDER_PAIR || orc_is_glm(m))       /* or in the wave order of the */
-                for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);     /* wave-per-chain kernel (d > 32) */
-            else
+            if (orc_is_glm(m) && d > 32)                                      /* or in the wave order of the */
+                nz = orc_dot_lanes(mom, d, 1);                                /* wave-per-chain kernels: the */
+            else if (order == 0 || order == ORC_ORDER_PAIR || orc_is_glm(m))  /* regression split step (d > 32, */
+                for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);     /* glm_ram_wave.hip), separable */
+            else                                                              /* targets (d > 32) */
                 nz = orc_dot(mom, m, order);
             for (int r = 0; r < d; ++r) {                                     /* S * rvec */
                 double a = 0.0;

@@ -622,6 +622,33 @@ def test_glm_ram_parity(gpu, kind, d):
     _assert_ram_factor(task, oc, d)
 
 
+@pytest.mark.parametrize("kind,d", [("linear", 33), ("logistic", 64), ("linear", 128), ("probit", 100),
+                                    ("logistic", 300), ("linear", 600), ("linear", 1024)])
+def test_glm_ram_wave_parity(gpu, kind, d):
+    """RAM on the regression targets for 32 < d <= 1024 (round 5): per step the regression eval kernel and the
+    wave-per-chain accept / factor-update kernel (glm_ram_wave.hip); samples, accept bits, final state, the
+    evaluation count and every factor bitwise against the oracle (|rvec|^2 in the 64-lane wave order); a tail wave,
+    several launches, a continuation."""
+    m = _glm_model(kind, d, n=40)
+    C = 37
+    r = mc.SerialMC(steps=12 if d <= 300 else 6, burnin=2, thinning=2)
+    task = (m * mc.RAM(0.5, 0.3) * r).batch(C, seed=55 + d, steps_per_launch=5)
+    chain = mc.run(task)
+    assert task.step_kernel.startswith("glm_ram_update<"), task.step_kernel
+    oc = orc.OracleChains(m, mc.RAM(0.5, 0.3), nchains=C, seed=55 + d)
+    s_ref, _, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, None, acc_ref, "ram")
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert task.evals == int(oc.n_evals.sum())
+    acc = chain.diagnostics["accept"]
+    assert 0 < acc.sum() < acc.size
+    _assert_ram_factor(task, oc, d)
+    c2 = mc.run(chain)
+    s2, _, a2 = oc.run(r)
+    assert_parity(c2, s2, None, a2, "ram")
+    _assert_ram_factor(task, oc, d)
+
+
 def test_ram_continue_spl_and_shards(gpu):
     """S lives on the device between runs; steps per launch and chain offsets are invisible."""
     d = 6
@@ -690,9 +717,9 @@ def test_ram_limits(gpu):
     m = _model("iso", 1025)
     with pytest.raises(mc.MCMCError, match="RAM is built for d <= 1024"):
         mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
-    m = _glm_model("linear", 40)
-    with pytest.raises(mc.MCMCError, match="RAM on regression targets is built for d <= 32"):
-        mc.run((m * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
+    with pytest.raises(mc.MCMCError, match="d <= 1024"):      # regression targets: RAM up to the models' own cap
+        m2 = mc.model(mc.LinearRegression(np.ones((20, 1025)), np.ones(20)), vars=np.zeros(1025), gradient=True)
+        mc.run((m2 * mc.RAM() * mc.SerialMC(steps=5)).batch(64))
 
 
 # ------------------------------------------------------------------ storeLeaps (HMC.jl:145-150, HMCDA.jl:110-117)
