@@ -336,7 +336,6 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
 #pragma unroll
         for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow1[glm_eta_off(m)];
         double y[4], bnd[4], term[4], rv[4];                    // y: the response, for the logistic model w (det_logi)
-        LogiState E[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
         if (LOGI) {
@@ -345,8 +344,10 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
         }
         // sub-stage j: the eta MFMAs [j KM / NSUB, (j+1) KM / NSUB), then stage st of one row (kGlmGroupRows
         // false) or of all four rows, four independent dependency chains (kGlmGroupRows true)
-        constexpr int NSTAGE = LOGI ? 3 : 1;
-        constexpr int NSUB = kGlmGroupRows ? NSTAGE : 4 * NSTAGE;
+        // logistic: one row's whole det_logi a sub-stage (its state stays in registers only that long)
+        constexpr int NSTAGE = 1;
+        constexpr bool GR = LOGI ? false : kGlmGroupRows;
+        constexpr int NSUB = GR ? NSTAGE : 4 * NSTAGE;
 #pragma unroll
         for (int j = 0; j < NSUB; ++j) {
 #pragma unroll
@@ -354,20 +355,16 @@ __device__ __forceinline__ double glm_eval1_tiles(const GlmArgs& a, const GlmPos
                 if (m + kLA < KM) av[m + kLA] = xrow1[glm_eta_off(m + kLA)];
                 eta_next = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x(m), eta_next, 0, 0, 0);
             }
-            const int st = kGlmGroupRows ? j : j >> 2;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (!kGlmGroupRows && r != (j & 3)) continue;
+                if (!GR && r != (j & 3)) continue;
                 if (LOGI) {
                     // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111)
-                    switch (st) {
-                        case 0:
-                            det_logi_s1(eta[r], y[r], E[r], sptab);
-                            ubnd = __builtin_fmax(ubnd, E[r].u + bnd[r]);            // the reference's -Inf
-                            break;
-                        case 1: det_logi_s2(E[r]); break;
-                        default: det_logi_fin(E[r], y[r], term[r], rv[r]); break;
-                    }
+                    LogiState E;
+                    det_logi_s1(eta[r], y[r], E, sptab);
+                    ubnd = __builtin_fmax(ubnd, E.u + bnd[r]);                    // the reference's -Inf
+                    det_logi_s2(E);
+                    det_logi_fin(E, y[r], term[r], rv[r]);
                 } else if (probit) {
                     glm_probit_obs(eta[r], y[r], term[r], rv[r]);
                 } else {
@@ -1402,16 +1399,21 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
             if (logi) {
                 // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111)
                 const double* LB = xslot(t) + BO;
-                LogiState E[4];
+                // two rows at a time: four rows' coefficient rows in flight at once spill the wave's registers
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    det_logi_s1(eta[r], y[r], E[r], sptab);
-                    ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * r]);           // the reference's -Inf
+                for (int h = 0; h < 4; h += 2) {
+                    LogiState E[2];
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        det_logi_s1(eta[h + r], y[h + r], E[r], sptab);
+                        ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * (h + r)]);   // the reference's -Inf
+                    }
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) det_logi_s2(E[r]);
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) det_logi_fin(E[r], y[h + r], term[h + r], rv[h + r]);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) det_logi_s2(E[r]);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) det_logi_fin(E[r], y[r], term[r], rv[r]);
             } else if (M.kind == MK_PROBIT) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) glm_probit_obs(eta[r], y[r], term[r], rv[r]);
