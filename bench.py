@@ -59,10 +59,11 @@ CONFIGS = {
                            "warmup, then the timed steps run at each chain's adapted dualLeapStep: a step is "
                            "round(len/eps) leapfrogs of that chain (HMCDA.jl:104)"),
     # round 5: the widened regression sizes (not BASELINE configs)
-    "linear1024": dict(model="linear", d=1024, n=4096, chains=65536 // 8, sampler="hmcda", steps=10, warmup=100,
+    "linear1024": dict(model="linear", d=1024, n=4096, chains=65536 // 8, sampler="hmcda", steps=4, warmup=30,
                        thinning=1, adapt=True,
                        desc="linear regression n=4096 d=1024 (config 5 at twice its width: eight 128-coordinate "
-                            "slices a chain tile), HMCDA(), 8,192 chains, adapted as linear512"),
+                            "slices a chain tile), HMCDA(), 8,192 chains; 30 untimed dual-averaging steps, then the "
+                            "timed steps at each chain's adapted step"),
     "ramlinear128": dict(model="linear", d=128, n=1000, chains=1 << 15, sampler="ram", steps=40, warmup=10,
                          thinning=10, desc="RAM(1., 0.3) on linear regression n=1000 d=128, 32,768 chains (the "
                                            "split step: regression eval kernel + wave-per-chain factor update)"),
@@ -393,6 +394,30 @@ def binomial_units(mc, model, C, local, config="binomial"):
     return out
 
 
+class _heartbeat:
+    """A progress line on stderr every 30 s while a long library call runs (ctypes releases the GIL), so a minutes-long
+    warmup (config 5 at d = 1024) is not mistaken for a hang."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        import threading
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self.stop.wait(self.every):
+            print(f"bench: {self.what} running, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+        return False
+
+
 def spawn_workers(args, argv):
     """`--gpus N` (N > 1) started as a plain process (no torchrun, WORLD_SIZE unset): re-launch this same command
     under torch.distributed.run with N processes, one per GPU, and return its exit code.  Runs before anything
@@ -485,8 +510,9 @@ def main():
         cfg = wr.cfg()
         ta = time.perf_counter()
         print(f"bench: warmup {W} steps", file=sys.stderr, flush=True)   # progress on stderr (stdout: the line)
-        _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(wout)))
-        torch.cuda.synchronize(dev)
+        with _heartbeat("warmup"):
+            _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(wout)))
+            torch.cuda.synchronize(dev)
         print(f"bench: warmup done in {time.perf_counter() - ta:.1f} s", file=sys.stderr, flush=True)
         if adaptive:
             eps = task.tuner_state()["step_bar"]
@@ -501,6 +527,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     cfg = runner.cfg()
+    hb = _heartbeat("timed run").__enter__()            # started before the clock: it only sleeps in between
     t0 = time.perf_counter()
     _lib.check(lib.mcmc_run_serialmc(h, ct.byref(cfg), ct.byref(out)))
     torch.cuda.synchronize(dev)
@@ -508,6 +535,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     T = time.perf_counter() - t0
+    hb.__exit__(None, None, None)
     print(f"bench: timed {K} steps in {T:.3f} s", file=sys.stderr, flush=True)
     kernel_ms = out.kernel_ms
     evals = task.evals - ev0
