@@ -67,9 +67,6 @@ constexpr bool kGlmGFence = GLM_GFENCE != 0;
 #ifndef GLM_WS_LA
 #define GLM_WS_LA 4
 #endif
-#ifndef GLM_WS_ETA2
-#define GLM_WS_ETA2 0
-#endif
 // NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
 
 struct GlmShape {
@@ -1345,17 +1342,6 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         double av[KM];
 #pragma unroll
         for (int m = 0; m < (kLA < KM ? kLA : KM); ++m) av[m] = xrow[glm_eta_off(m)];
-#if GLM_WS_ETA2
-        // experiment: two independent accumulators (even / odd k-slices), added at the end
-        f64x4 e0 = f64x4{0.0, 0.0, 0.0, 0.0}, e1 = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int m = 0; m < KM; ++m) {
-            if (m + kLA < KM) av[m + kLA] = xrow[glm_eta_off(m + kLA)];
-            if (m & 1) e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bx[m], e1, 0, 0, 0);
-            else e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bx[m], e0, 0, 0, 0);
-        }
-        return e0 + e1;
-#else
         f64x4 e = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int m = 0; m < KM; ++m) {
@@ -1363,7 +1349,6 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
             e = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bx[m], e, 0, 0, 0);
         }
         return e;
-#endif
     };
     auto g_of = [&](int64_t tt) {                              // G += X_tt^T r_tt (glm_eval1_tiles' G product)
         const f64x4 rv = Rq[256 * (tt & 1)];

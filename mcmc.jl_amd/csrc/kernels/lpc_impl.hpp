@@ -47,18 +47,6 @@ template <int NB, bool F, class M, bool US>
 __global__ __launch_bounds__(512, F && US ? 4 : 3) void lpp_rwm(KernelArgs a) {
     rwm_body<PairChain<NB, F, 512, kTabLds>, M, US>(a);
 }
-#ifndef LPP_PERSIST
-#define LPP_PERSIST 0
-#endif
-// experiment (LPP_PERSIST builds): the RWM pair kernel as a persistent grid, each workgroup running blocks of chains
-// vb = blockIdx.x, + gridDim.x, ... with the Box-Muller tables staged once
-template <int NB, bool F, class M, bool US>
-__global__ __launch_bounds__(512, F && US ? 4 : 3) void lpp_rwm_p(KernelArgs a, int64_t nvb) {
-    for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-        rwm_body<PairChain<NB, F, 512, kTabLds>, M, US>(a, vb, vb == (int64_t)blockIdx.x);
-        __syncthreads();                                  // the next turn's state loads after this turn's stores
-    }
-}
 template <int NB, bool F, class M>
 __global__ __launch_bounds__((lpp_mala_threads<NB, F>()), F ? 3 : 2) void lpp_mala(KernelArgs a) {
     mala_body<PairChain<NB, F, lpp_mala_threads<NB, F>(), kTabLds>, M>(a);
@@ -363,11 +351,7 @@ static hipError_t lpp_launch(const KernelArgs& a, hipStream_t st) {
     switch (a.sa.kind) {
         case SK_RWM:
             mcmc_note_step_kernel("lpp_rwm<%d, %s, %s, %s>", NBL, b, M::kName, us);
-            if (LPP_PERSIST && a.s.scale_uniform) {
-                const int64_t nvb = grid(512).x;
-                const int64_t np = nvb < 2 * 256 ? nvb : 2 * 256;                 // two workgroups a CU
-                lpp_rwm_p<NBL, F, M, true><<<dim3((unsigned)np), 512, 0, st>>>(a, nvb);
-            } else if (a.s.scale_uniform) lpp_rwm<NBL, F, M, true><<<grid(512), 512, 0, st>>>(a);
+            if (a.s.scale_uniform) lpp_rwm<NBL, F, M, true><<<grid(512), 512, 0, st>>>(a);
             else lpp_rwm<NBL, F, M, false><<<grid(512), 512, 0, st>>>(a);
             break;
         case SK_MALA:

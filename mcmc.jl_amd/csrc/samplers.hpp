@@ -219,12 +219,10 @@ struct PairChain {
     bool live;
     int d;
     int h;            // half: 0 (lanes 0-31) or 1 (lanes 32-63)
-    int64_t vb;       // the block of chains this workgroup runs now (blockIdx.x, or a persistent kernel's turn)
     BmTables<TAB, TH> bt;
-    __device__ PairChain(const StepArgs& s, bool defer = false, int64_t vblock = -1) {
+    __device__ PairChain(const StepArgs& s, bool defer = false) {
         const int lane = (int)(threadIdx.x & 63);
-        vb = vblock >= 0 ? vblock : (int64_t)blockIdx.x;
-        c = vb * kChainsPerBlock + (int64_t)(threadIdx.x >> 6) * 32 + (lane & 31);
+        c = (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)(threadIdx.x >> 6) * 32 + (lane & 31);
         h = lane >> 5;
         live = c < s.C;
         d = s.d;
@@ -242,7 +240,7 @@ struct PairChain {
     }
     __device__ __forceinline__ int64_t c_now() const {
         const uint32_t t = tid_now();
-        return vb * kChainsPerBlock + (int64_t)((t >> 6) * 32 + (t & 31));
+        return (int64_t)blockIdx.x * kChainsPerBlock + (int64_t)((t >> 6) * 32 + (t & 31));
     }
     __device__ __forceinline__ int coord(int k) const { return h * NC + k; }
     __device__ __forceinline__ bool valid(int k) const { return FULL || coord(k) < d; }
@@ -599,25 +597,18 @@ struct Keeper {
 };
 
 // ------------------------------------------------------------------ RWM
-// the chain policy of a kernel turn: staging deferred; PairChain also takes a persistent kernel's block of chains
-template <class P>
-__device__ __forceinline__ P make_chain(const StepArgs& s, int64_t vblock) {
-    if constexpr (P::kPairs) return P(s, true, vblock);
-    else return P(s, true);
-}
-
 // US: every coordinate has the same scale (s.scale1), held in one SGPR pair instead of d of them
 template <class P, class M, bool US = false>
-__device__ __forceinline__ void rwm_body(const KernelArgs& a, int64_t vblock = -1, bool stage_tables = true) {
+__device__ __forceinline__ void rwm_body(const KernelArgs& a) {
     const StepArgs& s = a.s;
-    const P p = make_chain<P>(s, vblock);
+    const P p(s, true);
     const M model(a.m);
     const Stream rs{s.key0, s.key1};
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
     double x[P::NC], sc[P::NC];
     p.load(a.st.x, s.ld, x);                                    // in flight while the tables are staged
     double lp = p.load_scalar(a.st.lp);
-    if (stage_tables) p.stage();
+    p.stage();
 #pragma unroll
     for (int k = 0; k < P::NC; ++k) sc[k] = p.valid(k) ? (US ? s.scale1 : s.scale[p.coord(k)]) : 0.0;
     AcceptDraw<P> ad;
