@@ -722,8 +722,15 @@ def main():
                     "launches": launches, "avg_launch_ms": avg_launch_s * 1e3,
                     "algorithmic_bytes_per_launch": fused / launches, "units_per_launch": units,
                     "survey_bytes": survey_bytes,
-                    "note": "no committed VALU profile of this kernel instance built from these sources "
-                            "(profiles/valu.json src_hash): HBM roofline of the fused design"}
+                    "note": ("RAM: the jump factor S (d(d+1)/2 doubles a chain) is read and written every step, "
+                             "so HBM binds (the factor update and matvec are 2 flops per 8-byte element)"
+                             if args.sampler == "ram" else
+                             "no committed VALU profile of this kernel instance built from these sources "
+                             "(profiles/valu.json src_hash): HBM roofline of the fused design")}
+        if C <= 64:
+            roof["binding"] = ("latency: a few-chain kernel runs each chain's steps as one dependent chain of "
+                               "operations (C <= 64: lpc_rwm_spec / lpc_rwm_la), so neither the VALU nor the HBM "
+                               "fraction is the bound; ms_per_step is the step's dependent-path latency")
     else:
         flop_per_eval = 4.0 * cfg0["n"] * d                           # eta = X beta, then X^T r
         flops = flop_per_eval * evals
