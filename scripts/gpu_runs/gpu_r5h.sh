@@ -1,10 +1,14 @@
-# round 4 fp64-datapath PMC passes of configs 5 and 3 for the final regression sources (bench.py's combined roofline)
+# round 5 final build, call B: fp64-datapath PMC passes of the regression configs (bench.py's fp64_combined roofline)
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r4q
+O=gpurun_out/r5h
 mkdir -p $O
 run() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name exit $rc"; [ $rc -eq 0 ] || exit $rc; }
 G="SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE;SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_LDS;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_LDS"
-PMC_GROUPS="$G" run pmc_log128 500 bash scripts/gpu_pmc.sh r4q_log128 --config logistic128 --steps 20 --warmup 2 --no-ess
-PMC_GROUPS="$G" run pmc_lin512 700 bash scripts/gpu_pmc.sh r4q_lin512 --config linear512 --steps 4 --warmup 100 --no-ess
+export PMC_GROUPS="$G"
+run pmc_log128 400 bash scripts/gpu_pmc.sh r5h_log128 --config logistic128 --steps 20 --warmup 2 --no-ess
+run pmc_lin512 700 bash scripts/gpu_pmc.sh r5h_lin512 --config linear512 --steps 4 --warmup 100 --no-ess
+run pmc_lin1024 700 bash scripts/gpu_pmc.sh r5h_lin1024 --config linear1024 --steps 2 --warmup 30 --no-ess
+run pmc_binomial 300 bash scripts/gpu_pmc.sh r5h_binomial --config binomial --steps 20 --no-ess
+run pmc_ramlinear 300 bash scripts/gpu_pmc.sh r5h_ramlinear --config ramlinear --steps 20 --no-ess
 echo all-done
