@@ -197,9 +197,10 @@ def test_bench_traffic_only_from_a_profile_of_the_same_kernel():
     import json
     bench = importlib.import_module("bench")
     t = json.load(open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "profiles", "traffic.json")))
-    key = next(k for k in t if k.startswith("logistic128|"))
-    assert bench.measured_traffic(key, t[key]["kernel"])["bytes_per_launch"] == t[key]["traffic_bytes"]
-    assert bench.measured_traffic(key, "glm_mala<8,1>") is None
+    for key in t:
+        assert bench.measured_traffic(key, t[key]["kernel"])["bytes_per_launch"] == t[key]["traffic_bytes"]
+        assert bench.measured_traffic(key, "glm_mala<8,1>") is None
+        assert os.path.exists(os.path.join(ROOT, t[key]["source"]))
     assert bench.measured_traffic("no-such-workload", "lpc_rwm") is None
     # the driver's exact command (bench.py --gpus 1 --steps 20 --warmup 5) has a committed profile
     dkey = "metric|d=32|chains=1048576|rwm|steps=20|thinning=10|spl=0"
