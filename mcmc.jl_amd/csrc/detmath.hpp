@@ -509,9 +509,9 @@ __device__ __forceinline__ double det_log_tab(double v, const double (*tab)[4] =
 // log(p) or log(1 - p)) makes the term -Inf where p rounds to 1 with y = 0 or to 0 with y = 1: u >= T(y)
 // (glm_layout.hpp logi_bound).  The kernels keep that: the tile carries b = -T(y) beside w and a lane whose max of u + b over its
 // observations is >= 0 contributes -Inf, so LLAcc puts the point out of support exactly where the reference does.
-// A NaN eta is not propagated (fmin): it needs a NaN or overflowing X beta, whose prior term already puts the chain
-// out of support (glm_finish; X and Y are finite by mcmc_model_create).  Stages as det_exp (the caller interleaves
-// work between them); oracle twin orc_logi.
+// A NaN eta is not propagated (fmin): it needs X beta to overflow with mixed signs, and mcmc_model_create refuses
+// data for which that can happen at any beta of finite prior density (row L1 norm x sqrt(DBL_MAX) prior_sigma <
+// 2^1022; X and Y finite).  Stages as det_exp (the caller interleaves work between them); oracle twin orc_logi.
 static __device__ const double kSoftplusTab[SP_NROWS][10] = {SP_TABLE_ROWS};
 
 

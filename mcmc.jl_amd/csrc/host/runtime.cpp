@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -424,6 +425,23 @@ extern "C" int mcmc_model_create(mcmc_ctx* ctx, const mcmc_model_desc* desc, mcm
                 if (!std::isfinite(desc->X[i])) return bail(fail(MCMC_E_INVALID_ARG, "X must be finite"));
             for (int64_t i = 0; i < desc->n; ++i)
                 if (!std::isfinite(desc->Y[i])) return bail(fail(MCMC_E_INVALID_ARG, "Y must be finite"));
+            // The logistic / probit terms clamp |eta| into their tables (det_logi, the normal log-cdf twins), so a
+            // NaN eta would not reach LLAcc's non-finite rule as it does in the reference (a NaN term makes the sum
+            // NaN and the point out of support, modelparser.jl:64-72).  eta is NaN only when X vars overflows with
+            // mixed signs: every partial sum of row i is bounded by |vars|_inf |X_i|_1, and a vars whose prior term
+            // is finite has |vars|_inf < sqrt(DBL_MAX) prior_sigma.  Data for which that product can reach 2^1022
+            // (rows with L1 norm ~1e154 / prior_sigma) are refused here instead of clamped in the kernels.
+            if (desc->kind == MCMC_MODEL_LOGISTIC || desc->kind == MCMC_MODEL_PROBIT) {
+                double l1max = 0.0;
+                for (int64_t i = 0; i < desc->n; ++i) {
+                    double l1 = 0.0;
+                    for (int k = 0; k < d; ++k) l1 += std::fabs(desc->X[i * (int64_t)d + k]);
+                    l1max = std::max(l1max, l1);
+                }
+                if (!(l1max * (std::sqrt(DBL_MAX) * desc->prior_sigma) < 0x1p1022))
+                    return bail(fail(MCMC_E_UNSUPPORTED, "covariates too large: X * vars can overflow to NaN at a "
+                                                         "parameter vector of finite prior density"));
+            }
             // the logistic model's tile columns hold w = s (2y - 1) (s the link sign) instead of y and the bounds
             // -T(y) where the reference's p rounds to 1 or 0 (detmath.hpp det_logi, logi_bound)
             std::vector<double> Yw, Bw;

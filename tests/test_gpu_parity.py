@@ -465,6 +465,22 @@ def test_logistic_out_of_support_rejects(gpu):
     assert_parity(ch, s, g, acc, "rwm")
 
 
+@pytest.mark.parametrize("kind", ["logistic", "probit"])
+def test_covariates_that_can_overflow_to_nan_are_refused(gpu, kind):
+    """X vars overflowing with mixed signs gives a NaN eta, which the reference's LLAcc turns into -Inf; the kernels
+    clamp |eta| into their tables, so mcmc_model_create refuses data whose row L1 norm times the largest |vars| of
+    finite prior density can reach 2^1022 (runtime.cpp), and accepts the same rows scaled into range."""
+    from mcmchip import _lib
+    X = np.array([[1.0, 1e200], [1.0, -1e200], [1.0, 3.0]])
+    Y = np.array([0.0, 1.0, 1.0])
+    T = mc.LogisticRegression if kind == "logistic" else mc.ProbitRegression
+    m = mc.model(T(X, Y), vars=np.zeros(2), gradient=True)
+    with pytest.raises(_lib.MCMCError, match="overflow to NaN"):
+        mc.run((m * mc.RWM(0.1) * mc.SerialMC(steps=4)).batch(64, seed=1))
+    m = mc.model(T(X * 1e-100, Y), vars=np.zeros(2), gradient=True)
+    mc.run((m * mc.RWM(0.1) * mc.SerialMC(steps=4)).batch(64, seed=1))
+
+
 @pytest.mark.parametrize("sname", ["rwm", "hmc"])
 def test_glm_nonzero_init_few_coords_many_chains(gpu, sname):
     """d << C with a non-zero start: the coordinate-major state must be broadcast per coordinate row."""
