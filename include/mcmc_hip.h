@@ -22,7 +22,8 @@
  *   run(t::MCMCTask) / run_serialmc  runners.jl:7-11,45,    mcmc_run_serialmc
  *                                    SerialMC.jl:37-85
  *   run(c::MCMCChain) (continue)     runners.jl:14          mcmc_run_serialmc again on the same chains
- *   resume(c; steps)                 SerialMC.jl:93-97      mcmc_chains_reset + mcmc_run_serialmc
+ *   resume(c; steps)                 SerialMC.jl:93-97      a new batch (mcmc_chains_create) on fresh global
+ *                                                           chain ids + mcmc_run_serialmc
  *   MCMCChain fields                 MCMC.jl:58-80          mcmc_outputs (samples, gradients,
  *                                                           accept bits, runtime)
  *   acceptance(chain)                summary.jl:6-15        computed by the host from accept bits
@@ -215,6 +216,13 @@ int mcmc_chains_evals(mcmc_chains* chains, int64_t* evals);
 int mcmc_chains_ram_factor(mcmc_chains* chains, double* S);
 /* steps fused per kernel launch (0 = whole run in one launch, the default). */
 int mcmc_chains_set_steps_per_launch(mcmc_chains* chains, int64_t steps_per_launch);
+/* The burnin the samplers' adaptation sees, apart from the kept range of mcmc_run_serialmc.  The reference's
+ * tuners read the task's own runner: EmpiricalMALATune / EmpiricalHMCTune adapt while i <= runner.burnin
+ * (MALA.jl:116, HMC.jl:167) and HMCDA dual-averages while i < runner.burnin (HMCDA.jl:133-141), i the sampler's
+ * step counter.  A host that keeps every step of a run and applies the kept range itself (a Julia Task producing
+ * one MCMCSample per consume, in chunks: julia/mcmc_jl_hook.jl) sets the task runner's burnin here.  -1 (the
+ * default): each run's own runner->burnin.  Copied by mcmc_chains_fork. */
+int mcmc_chains_set_tuner_burnin(mcmc_chains* chains, int64_t burnin);
 /* store gradients of kept samples for gradient samplers (default 1, SerialMC.jl:51-53) */
 int mcmc_chains_set_store_gradients(mcmc_chains* chains, int32_t store);
 /* pre-size the library's own output buffers for runs keeping up to nkept steps (staging of the

@@ -113,6 +113,7 @@ struct mcmc_chains {
     int64_t steps_done = 0;
     int64_t spl = 0;                 // steps per launch (0: whole run)
     int store_grads = 1;
+    int64_t tuner_burnin = -1;       // the tuners' burnin (mcmc_chains_set_tuner_burnin); -1: the run's runner burnin
     DevBuf out_samples, out_grads, out_bits, out_tmp, stage_samples, stage_grads;
     DevBuf order_buf;                // regression HMC / HMCDA: chain slot -> chain (StepArgs.order)
     std::vector<int32_t> h_order;
@@ -981,6 +982,7 @@ extern "C" int mcmc_chains_fork(mcmc_chains* src, int64_t first, int64_t count, 
     c->steps_done = src->steps_done;
     c->spl = src->spl;
     c->store_grads = src->store_grads;
+    c->tuner_burnin = src->tuner_burnin;
     *out = c;
     return MCMC_OK;
 }
@@ -1073,6 +1075,13 @@ extern "C" int mcmc_chains_step_kernel(mcmc_chains* c, char* buf, int64_t cap) {
 extern "C" int mcmc_chains_set_steps_per_launch(mcmc_chains* c, int64_t spl) {
     if (!c || spl < 0) return fail(MCMC_E_INVALID_ARG, "bad argument");
     c->spl = spl;
+    return MCMC_OK;
+}
+
+extern "C" int mcmc_chains_set_tuner_burnin(mcmc_chains* c, int64_t burnin) {
+    if (!c) return fail(MCMC_E_INVALID_ARG, "chains is NULL");
+    if (burnin < -1) return fail(MCMC_E_INVALID_ARG, "tuner burnin must be >= 0, or -1 (the runner's burnin)");
+    c->tuner_burnin = burnin;
     return MCMC_OK;
 }
 
@@ -1237,7 +1246,7 @@ int mcmc_run_serialmc_ld(mcmc_chains* c, const mcmc_runner_cfg* r, mcmc_outputs*
     s.burnin = r->burnin;
     s.thinning = r->thinning;
     s.len = r->len;
-    s.tuner_burnin = r->burnin;
+    s.tuner_burnin = c->tuner_burnin >= 0 ? c->tuner_burnin : r->burnin;   // MALA.jl:116, HMC.jl:167, HMCDA.jl:133
     s.scale = c->d_scale_eff;
     s.scale1 = c->scale1;
     s.scale_uniform = c->scale_uniform;

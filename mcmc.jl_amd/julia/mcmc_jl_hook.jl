@@ -19,18 +19,29 @@
 #                                                  not yet started) run as ONE chain batch, one mcmc_run_serialmc;
 #                                                  each returned MCMCChain's task continues its own chain.  Any
 #                                                  other array goes through the reference's dispatch as before;
-#   prun(t::Array{MCMCTask})    runners.jl:35-42 -- redefined likewise: like GPU tasks as one batch, then stopped
-#                                                  (run_serialmc_exit); other arrays pmap as before.
+#                                                  With SeqMC runners, GPU targets run as one mcmc_run_seqmc (one
+#                                                  chain batch per target, a chain per particle) instead of
+#                                                  run_seqmc's reset + consume per particle (SeqMC.jl:39-122);
+#   prun(t::Array{MCMCTask})    runners.jl:35-42 -- redefined likewise: like GPU tasks as one batch split over every
+#                                                  visible GPU (mcmc_group_*), then stopped (run_serialmc_exit);
+#                                                  other arrays pmap as before;
+#   ess(cs::Array{MCMCChain})   ess.jl:6-10      -- a new method (the reference's ess(c::MCMCChain) is untouched):
+#                                                  the ESS of every chain of a GPU batch in one mcmc_stats_ess call.
+# Runner semantics.  A GPU task produces every step (run_serialmc applies the kept range itself), in chunks of at
+# most the task runner's len; the samplers' adaptation reads the task's own runner (MALA.jl:116, HMC.jl:167,
+# HMCDA.jl:133-141), so the task runner's burnin is set as the chains' tuner burnin (mcmc_chains_set_tuner_burnin)
+# apart from the chunks' kept range.  All tasks of one MCMCHipModel share one uploaded model per device.
 # Random streams.  The reference's tasks draw from Julia's global RNG as they run, so every spun task samples a
 # chain of its own.  A GPU chain's stream is (Philox key, global chain id), so the mirror of the global RNG is
 # hip_stream: a key plus a cursor over chain ids (hip_srand(seed) restarts it); a task takes its id when it first
-# runs.
+# runs.  Drawn keys carry the top bit (hip_key), explicit seeds of the plain binding (MCMCHip.jl) do not, so the two
+# never share a stream.
 # Text only in this repository: the image has no Julia.  Struct layouts mirror include/mcmc_hip.h field for field
 # (tests/test_api_cpu.py::test_julia_hook_structs_mirror_header checks the field lists against the header).
 
 const hiplib = haskey(ENV, "MCMCHIP_LIB") ? ENV["MCMCHIP_LIB"] : "libmcmc_hip"
 
-export MCMCHipModel, hipmodel, hip_run_batch, hip_run_arrays, hip_srand
+export MCMCHipModel, hipmodel, hip_run_batch, hip_run_arrays, hip_srand, hip_ess
 
 # ---- C structs (include/mcmc_hip.h), isbits, C layout
 immutable HipModelDesc            # mcmc_model_desc
@@ -53,6 +64,9 @@ type HipOutputs                   # mcmc_outputs (the library writes runtime_s, 
   samples::Ptr{Float64}; gradients::Ptr{Float64}; accept_bits::Ptr{Uint64}
   final_x::Ptr{Float64}; final_lp::Ptr{Float64}; on_device::Int32
   runtime_s::Float64; kernel_ms::Float64; nkept::Int64
+end
+immutable HipSeqMCCfg             # mcmc_seqmc_cfg
+  steps::Int64; burnin::Int64; trigger::Float64
 end
 
 const HIP_MODEL_KINDS = {:isonormal_dot => 1, :normal => 2, :logistic => 3, :linear => 4, :absnormal => 5, :dist => 6,
@@ -175,7 +189,7 @@ type HipChains
   model::HipModelHandle
   d::Int
   nchains::Int
-  function HipChains(mh::HipModelHandle, cfg::HipSamplerCfg, d::Int, nchains::Int, seed::Int, offset::Int)
+  function HipChains(mh::HipModelHandle, cfg::HipSamplerCfg, d::Int, nchains::Int, seed::Uint64, offset::Int)
     h = Array(Ptr{Void}, 1)
     hipcheck(ccall((:mcmc_chains_create, hiplib), Cint,
                    (Ptr{Void}, Ptr{HipSamplerCfg}, Int64, Int64, Uint64, Ptr{Float64}, Ptr{Ptr{Void}}),
@@ -205,17 +219,34 @@ end
 const hip_contexts = Dict{Int, HipContext}()
 hip_context(dev::Int) = haskey(hip_contexts, dev) ? hip_contexts[dev] : (hip_contexts[dev] = HipContext(dev))
 
-hip_chains(m::MCMCHipModel, s::MCMCSampler, nchains::Int, seed::Int, offset::Int) =
-  HipChains(HipModelHandle(hip_context(m.device), m), hip_sampler(s), m.size, nchains, seed, offset)
+# the tuners' burnin of a task's chains: its own runner's (MALA.jl:116, HMC.jl:167, HMCDA.jl:133-141)
+hip_set_tuner_burnin!(ch::HipChains, burnin::Int) =
+  hipcheck(ccall((:mcmc_chains_set_tuner_burnin, hiplib), Cint, (Ptr{Void}, Int64), ch.h, burnin))
+hip_tuner_burnin(r::MCMCRunner) = (isa(r, SerialMC) || isa(r, SeqMC)) ? r.burnin : 0
+
+# one uploaded model (X, Y, init, scale on the device) per MCMCHipModel object, shared by every task spun from it;
+# held weakly, so it goes with the model (a task's chains keep their handle alive while they live)
+const hip_model_handles = WeakKeyDict()
+function hip_model_handle(m::MCMCHipModel)
+  if !haskey(hip_model_handles, m) || hip_model_handles[m].ctx.h != hip_context(m.device).h
+    hip_model_handles[m] = HipModelHandle(hip_context(m.device), m)
+  end
+  hip_model_handles[m]
+end
+
+hip_chains(m::MCMCHipModel, s::MCMCSampler, nchains::Int, seed::Uint64, offset::Int) =
+  HipChains(hip_model_handle(m), hip_sampler(s), m.size, nchains, seed, offset)
 
 # ---- the global stream (see the header): hip_draw(n) takes n consecutive global chain ids; ids are 32-bit (the
-#      Philox counter's chain word), so a cursor that would pass 2^32 moves on to the next key
+#      Philox counter's chain word), so a cursor that would pass 2^32 moves on to the next key.  The Philox key of a
+#      drawn stream is hip_key(seed): the top bit set, a key space no explicit seed (< 2^63) reaches
 type HipStream
   seed::Int
   next::Int
 end
 const hip_stream = HipStream(1, 0)
 hip_srand(seed::Int) = (hip_stream.seed = seed; hip_stream.next = 0; nothing)
+hip_key(seed::Int) = (uint64(seed) & 0x7fffffffffffffff) | 0x8000000000000000
 function hip_draw(n::Int)
   if hip_stream.next + n > 2^32
     hip_stream.seed += 1
@@ -223,7 +254,7 @@ function hip_draw(n::Int)
   end
   first = hip_stream.next
   hip_stream.next += n
-  (hip_stream.seed, first)
+  (hip_key(hip_stream.seed), first)
 end
 
 # one mcmc_run_serialmc of `len` steps, rows (burnin+1):thinning:len kept: samples / gradients [nkept*d*C]
@@ -241,14 +272,19 @@ type HipRun
 end
 hip_accept(o::HipRun, j::Int, c::Int) = (o.bits[div(c - 1, 64) + 1, j] >> ((c - 1) % 64)) & 1 == 1
 
-function hip_run!(ch::HipChains, burnin::Int, thinning::Int, len::Int, grads::Bool, cap::Int=-1)
-  nk = length((burnin + 1):thinning:len)
-  C, d, nw = ch.nchains, ch.d, div(ch.nchains + 63, 64)
+function hip_out_arrays(C::Int, d::Int, nk::Int, grads::Bool)
   x = Array(Float64, C, d, nk)
   g = grads ? Array(Float64, C, d, nk) : Array(Float64, 0, 0, 0)
-  bits = Array(Uint64, nw, nk)
+  bits = zeros(Uint64, div(C + 63, 64), nk)
   fx = Array(Float64, C, d)
   flp = Array(Float64, C)
+  x, g, bits, fx, flp
+end
+
+function hip_run!(ch::HipChains, burnin::Int, thinning::Int, len::Int, grads::Bool, cap::Int=-1)
+  nk = length((burnin + 1):thinning:len)
+  C, d = ch.nchains, ch.d
+  x, g, bits, fx, flp = hip_out_arrays(C, d, nk, grads)
   leaps = Dict()
   if cap >= 0
     for k in (:pars, :grad, :m); leaps[k] = Array(Float64, C, d, cap + 1, nk); end
@@ -263,6 +299,51 @@ function hip_run!(ch::HipChains, burnin::Int, thinning::Int, len::Int, grads::Bo
   hipcheck(ccall((:mcmc_run_serialmc, hiplib), Cint, (Ptr{Void}, Ptr{HipRunnerCfg}, Ptr{HipOutputs}),
                  ch.h, [HipRunnerCfg(burnin, thinning, len)], &out))
   HipRun(x, g, bits, fx, flp, out.runtime_s, leaps)
+end
+
+# ---- one node's GPUs (mcmc_group_*, the prun replacement, runners.jl:35-42): one batch of n chains split into
+#      contiguous 64-chain-aligned blocks, one per device, every block's step loop concurrently, each block's outputs
+#      copied device -> host into its columns of the arrays; bit-identical to one context running every chain
+type HipGroup
+  h::Ptr{Void}
+  function HipGroup(devs::Vector{Int32})
+    h = Array(Ptr{Void}, 1)
+    hipcheck(ccall((:mcmc_group_create, hiplib), Cint, (Ptr{Int32}, Int32, Ptr{Ptr{Void}}), devs, length(devs), h))
+    g = new(h[1])
+    finalizer(g, x -> (x.h == C_NULL || ccall((:mcmc_group_destroy, hiplib), Cint, (Ptr{Void},), x.h); x.h = C_NULL))
+    g
+  end
+end
+function hip_devices()
+  n = Array(Cint, 1)
+  hipcheck(ccall((:mcmc_device_count, hiplib), Cint, (Ptr{Cint},), n))
+  Int32[0:(n[1] - 1)]
+end
+const hip_groups = Dict{Vector{Int32}, HipGroup}()
+hip_group(devs::Vector{Int32}) = haskey(hip_groups, devs) ? hip_groups[devs] : (hip_groups[devs] = HipGroup(devs))
+
+function hip_run_group(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, n::Int, seed::Uint64, first::Int,
+                       devs::Vector{Int32})
+  g = hip_group(devs)
+  Xr = isempty(m.X) ? Float64[] : vec(m.X')
+  desc = [hip_desc(m, Xr)]                                # model uploaded once per device by the library
+  h = Array(Ptr{Void}, 1)
+  hipcheck(ccall((:mcmc_group_chains_create, hiplib), Cint,
+                 (Ptr{Void}, Ptr{HipModelDesc}, Ptr{HipSamplerCfg}, Int64, Int64, Uint64, Ptr{Float64}, Ptr{Ptr{Void}}),
+                 g.h, desc, [hip_sampler(s)], n, first, seed, convert(Ptr{Float64}, C_NULL), h))
+  length(Xr) + length(m.Y) + length(m.init) + length(m.scale)   # the descriptor's arrays stay rooted to here
+  try
+    x, gr, bits, fx, flp = hip_out_arrays(n, m.size, length(r.r), has_grads(s))
+    out = HipOutputs(pointer(x), has_grads(s) ? pointer(gr) : convert(Ptr{Float64}, C_NULL), pointer(bits),
+                     pointer(fx), pointer(flp), 0, 0., 0., 0)
+    gather = Array(Float64, 1)
+    hipcheck(ccall((:mcmc_group_run_serialmc, hiplib), Cint,
+                   (Ptr{Void}, Ptr{HipRunnerCfg}, Ptr{HipOutputs}, Ptr{Float64}),
+                   h[1], [HipRunnerCfg(r.burnin, r.thinning, r.len)], &out, gather))
+    HipRun(x, gr, bits, fx, flp, out.runtime_s, Dict())
+  finally
+    ccall((:mcmc_group_chains_destroy, hiplib), Cint, (Ptr{Void},), h[1])   # prun's tasks come back stopped
+  end
 end
 
 has_grads(s::MCMCSampler) = isa(s, MALA) || isa(s, HMC) || isa(s, HMCDA)
@@ -282,10 +363,11 @@ end
 type HipTaskState
   model::MCMCHipModel
   sampler::MCMCSampler
+  runner::MCMCRunner                  # the task's runner: its burnin drives the tuners, its len the chunk length
   chains::Union(HipChains, Nothing)   # the task's one GPU chain, made on first use
   src::Union(HipChains, Nothing)      # after a batched run: the batch, whose chain `first` this task continues
   first::Int
-  seed::Int
+  seed::Uint64
   offset::Int                         # global chain id; -1 until drawn
   stopped::Bool
   buf::Union(HipRun, Nothing)         # chunk mode: steps run ahead on the GPU, produced one by one
@@ -294,8 +376,8 @@ type HipTaskState
   x::Vector{Float64}
   lp::Float64
 end
-HipTaskState(m::MCMCHipModel, s::MCMCSampler) =
-  HipTaskState(m, s, nothing, nothing, 0, 0, -1, false, nothing, 0, false, Float64[], NaN)
+HipTaskState(m::MCMCHipModel, s::MCMCSampler, r::MCMCRunner) =
+  HipTaskState(m, s, r, nothing, nothing, 0, uint64(0), -1, false, nothing, 0, false, Float64[], NaN)
 const hip_tasks = WeakKeyDict()
 
 function hip_ensure!(st::HipTaskState)
@@ -308,6 +390,9 @@ function hip_ensure!(st::HipTaskState)
     st.seed, st.offset = hip_draw(1)
     st.chains = hip_chains(st.model, st.sampler, 1, st.seed, st.offset)
   end
+  # every step is kept by the chunk runs (hip_produce_loop), so the adaptation window is set apart: the task
+  # runner's burnin (MALA.jl:116, HMC.jl:167, HMCDA.jl:133-141)
+  hip_set_tuner_burnin!(st.chains, hip_tuner_burnin(st.runner))
   st.chains
 end
 
@@ -327,9 +412,14 @@ end
 #      from GPU runs of `chunk` steps (every step kept; plogtarget / pars / logtarget NaN: run_serialmc reads only
 #      ppars, pgrads and diagnostics), or, after MCMC.reset, from single GPU steps with their log-targets.
 #      A continuation (run(c), runners.jl:14) keeps consuming the same task, i.e. the same GPU chain.
+#      A chunk is at most the task runner's len (one run(t) consumes exactly len steps: nothing runs ahead of what
+#      run_serialmc takes), capped at hip_chunk; a task whose runner is not SerialMC (consumed one sample at a time
+#      by run_seqmc / run_serialtempmc) steps one at a time.
 const hip_chunk = 1000
-hip_chunk_len(st::HipTaskState, cap::Int) =
-  cap < 0 ? hip_chunk : max(1, min(hip_chunk, div(1 << 28, 8 * (cap + 1) * (3 * st.model.size + 2))))
+function hip_chunk_len(st::HipTaskState, cap::Int)
+  n = isa(st.runner, SerialMC) ? min(hip_chunk, st.runner.len) : 1
+  cap < 0 ? n : max(1, min(n, div(1 << 28, 8 * (cap + 1) * (3 * st.model.size + 2))))
+end
 
 function hip_produce_loop(st::HipTaskState)
   task_local_storage(:reset, (resetPars::Vector{Float64}) -> hip_reset!(st, resetPars))
@@ -363,7 +453,7 @@ end
 
 function spinTask(m::MCMCHipModel, s::MCMCSampler, r::MCMCRunner)
   hip_sampler(s)                                         # refuse unsupported configurations now, as the ctor would
-  st = HipTaskState(m, s)
+  st = HipTaskState(m, s, r)
   task = Task(() -> hip_produce_loop(st))
   hip_tasks[task] = st
   MCMCTask(task, m, s, r)
@@ -420,13 +510,19 @@ end
 
 # one mcmc_run_serialmc for every task of t (consecutive global chain ids from the stream); task k then continues
 # chain k (a fork of the batch's state on its first use) or, with stop (prun), is stopped (run_serialmc_exit)
-function hip_run_tasks(t::Array{MCMCTask}, stop::Bool)
+#      (prun: over the devices `devs` as one mcmc_group when there are several; storeLeaps records stay on one device)
+function hip_run_tasks(t::Array{MCMCTask}, stop::Bool, devs::Vector{Int32}=Int32[])
   m, s, r = t[1].model, t[1].sampler, t[1].runner
   n = length(t)
   seed, first = hip_draw(n)
-  ch = hip_chains(m, s, n, seed, first)
-  cap = hip_store_leaps(s) ? hip_leaps_cap(s) : -1
-  o = hip_run!(ch, r.burnin, r.thinning, r.len, has_grads(s), cap)
+  ch = nothing
+  if stop && length(devs) > 1 && !hip_store_leaps(s)
+    o = hip_run_group(m, s, r, n, seed, first, devs)
+  else
+    ch = hip_chains(m, s, n, seed, first)
+    cap = hip_store_leaps(s) ? hip_leaps_cap(s) : -1
+    o = hip_run!(ch, r.burnin, r.thinning, r.len, has_grads(s), cap)
+  end
   res = Array(MCMCChain, size(t))
   for k in 1:n
     st = hip_tasks[t[k].task]
@@ -447,6 +543,7 @@ function run(t::Array{MCMCTask}; args...)
   lastrunner = t[end].runner
   @assert all(map(x -> isa(x.runner, typeof(lastrunner)), t)) "Runners do not have the same runner type"
   isa(lastrunner, SerialMC) && hip_batchable(t) && return hip_run_tasks(t, false)
+  isa(lastrunner, SeqMC) && hip_seqmc_able(t) && return hip_run_seqmc(t; args...)
   if isa(lastrunner, SerialMC)
     res = Array(MCMCChain, size(t))
     for i in 1:length(t); res[i] = run(t[i]); end
@@ -461,8 +558,89 @@ function prun(t::Array{MCMCTask}; args...)
   lastrunner = t[end].runner
   @assert all(map(x -> isa(x.runner, typeof(lastrunner)), t)) "Runners do not have the same runner type"
   isa(lastrunner, SerialMC) || return nothing
-  hip_batchable(t) && return hip_run_tasks(t, true)
+  hip_batchable(t) && return hip_run_tasks(t, true, hip_devices())
   pmap(run_serialmc_exit, t)
+end
+
+# ---- SeqMC (SeqMC.jl:39-122) on the GPU: GPU targets, none started, one parameter size
+function hip_seqmc_able(t::Array{MCMCTask})
+  isempty(t) && return false
+  for x in t
+    (isa(x.model, MCMCHipModel) && haskey(hip_tasks, x.task)) || return false
+    st = hip_tasks[x.task]
+    (st.chains == nothing && st.src == nothing && !st.stopped) || return false
+  end
+  true
+end
+
+# Philox key of target k's chains (mcmchip.seqmc.target_seed on the drawn key, kept in the drawn key space)
+hip_target_key(seed::Uint64, k::Int) = ((seed + uint64(k + 1) * 0x9e3779b97f4a7c15) & 0x7fffffffffffffff) |
+                                       0x8000000000000000
+
+# run_seqmc(targets; particles) as one mcmc_run_seqmc: particle n is chain n of every target's chain batch; per outer
+# step and target every particle is reset into the target (MCMC.reset) and advanced one step of its sampler, the
+# weights updated and, when var(W) < trigger, the particles resampled -- on the device, no host round trip inside the
+# loop.  The chain is the reference's: samples (steps - burnin) * npart rows, step-major; diagnostics "weigths" (sic,
+# SeqMC.jl:119) and "particle"; its range the reference's own (burnin+1):1:((steps-burnin)*npart) (SeqMC.jl:116).
+# The particles' chains and the resampling draws come from the global stream (hip_draw): a fresh population stream.
+function hip_run_seqmc(targets::Array{MCMCTask}; particles::Vector{Vector{Float64}} = [[randn()] for i in 1:100])
+  ntargets = length(targets)
+  npart = length(particles)
+  tsize = targets[end].model.size
+  r = targets[end].runner
+  @assert all(map(t -> t.model.size, targets) .== tsize) "Models do not have the same parameter vector size"
+  @assert all(map(p -> length(p), particles) .== tsize) "particles must have $tsize coordinates"
+  seed, first = hip_draw(npart)
+  chs = HipChains[HipChains(hip_model_handle(targets[k].model), hip_sampler(targets[k].sampler), tsize, npart,
+                            hip_target_key(seed, k - 1), first) for k in 1:ntargets]
+  P = Float64[particles[n][j] for n in 1:npart, j in 1:tsize]           # [d][npart] in C order
+  nst = r.steps - r.burnin
+  S = Array(Float64, npart, tsize, nst)                                  # [nst][d][npart]
+  W = Array(Float64, npart, nst)                                         # [nst][npart]
+  F = zeros(Int32, ntargets, r.steps)                                    # resampled flags [steps][ntargets]
+  rt = Array(Float64, 1)
+  hipcheck(ccall((:mcmc_run_seqmc, hiplib), Cint,
+                 (Ptr{Ptr{Void}}, Int32, Int64, Ptr{Float64}, Ptr{HipSeqMCCfg}, Uint64, Int32, Ptr{Float64},
+                  Ptr{Float64}, Ptr{Int32}, Ptr{Float64}),
+                 Ptr{Void}[c.h for c in chs], ntargets, npart, P, [HipSeqMCCfg(r.steps, r.burnin, r.trigger)], seed,
+                 0, S, W, F, rt))
+  M = Array(Float64, nst * npart, tsize)
+  for i in 1:nst, j in 1:tsize, n in 1:npart
+    M[(i - 1) * npart + n, j] = S[n, j, i]
+  end
+  MCMCChain((r.burnin + 1):1:((r.steps - r.burnin) * npart), DataFrame(M, hip_colnames(targets[end].model)),
+            DataFrame(), {"weigths" => vec(W), "particle" => rep([1:npart], nst), "resampled" => F'}, targets, rt[1])
+end
+
+# ---- ESS on the device (ess.jl:6-10 with var.jl's IMSE / IPSE / batch means; mcmc_stats_ess)
+const HIP_VTYPES = {:imse => 1, :ipse => 2, :bm => 3}
+
+# samples as hip_run_arrays returns them, (C, d, nkept): ESS and the vtype variance of the mean, each (C, d)
+function hip_ess(x::Array{Float64, 3}; vtype::Symbol=:imse, maxlag::Int=0, batchlen::Int=100, device::Int=0)
+  @assert haskey(HIP_VTYPES, vtype) "Unknown ESS type $vtype"
+  C, d, nk = size(x)
+  e, v = Array(Float64, C, d), Array(Float64, C, d)
+  hipcheck(ccall((:mcmc_stats_ess, hiplib), Cint,
+                 (Ptr{Void}, Ptr{Float64}, Int64, Int64, Int64, Int32, Int64, Int64, Int32, Ptr{Float64}, Ptr{Float64}),
+                 hip_context(device).h, x, nk, d, C, HIP_VTYPES[vtype], maxlag, batchlen, 0, e, v))
+  e, v
+end
+
+# ess(c) of every chain of an array; chains of GPU tasks with equal shapes go to the device in one call, as ess(c)
+# would give each (ess.jl:6-10: nrow * var_iid / var_vtype over every column); anything else chain by chain
+function ess(cs::Array{MCMCChain}; vtype::Symbol=:imse, maxlag::Int=0, batchlen::Int=100)
+  gpu = !isempty(cs) && all(c -> isa(c.task, MCMCTask) && isa(c.task.model, MCMCHipModel), cs)
+  if gpu
+    nk, d = size(cs[1].samples)
+    gpu = all(c -> size(c.samples) == (nk, d), cs)
+  end
+  if !gpu
+    return [vtype == :bm ? ess(c; vtype=vtype, batchlen=batchlen) :
+            maxlag > 0 ? ess(c; vtype=vtype, maxlag=maxlag) : ess(c; vtype=vtype) for c in cs]
+  end
+  x = Float64[cs[c].samples[k, j] for c in 1:length(cs), j in 1:d, k in 1:nk]
+  e, _ = hip_ess(x; vtype=vtype, maxlag=maxlag, batchlen=batchlen, device=cs[1].task.model.device)
+  [vec(e[c, :]) for c in 1:length(cs)]
 end
 
 # nchains independent chains as one batch, each returned MCMCChain's task continuing its own chain
@@ -473,7 +651,9 @@ hip_run_batch(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, nchains::Int) =
 # DataFrames would not fit in host memory; the chains come from the global stream
 function hip_run_arrays(m::MCMCHipModel, s::MCMCSampler, r::SerialMC, nchains::Int)
   seed, first = hip_draw(nchains)
-  o = hip_run!(hip_chains(m, s, nchains, seed, first), r.burnin, r.thinning, r.len, has_grads(s))
+  devs = hip_devices()
+  o = (length(devs) > 1 && nchains >= 64 * length(devs)) ? hip_run_group(m, s, r, nchains, seed, first, devs) :
+      hip_run!(hip_chains(m, s, nchains, seed, first), r.burnin, r.thinning, r.len, has_grads(s))
   nk = size(o.x, 3)
   o.x, o.g, Bool[hip_accept(o, j, c) for j in 1:nk, c in 1:nchains], o.runtime
 end

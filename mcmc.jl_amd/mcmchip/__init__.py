@@ -9,7 +9,7 @@ from .api import (  # noqa: F401
     OrnsteinUhlenbeck, ou_series,
     MCMCLikelihoodModel, model,
     RWM, MALA, HMC, HMCDA, RAM, EmpMCTuner, EmpiricalMCMCTuner, SerialMC, MCMCTask, MCMCChain,
-    run, prun, resume, reset, srand, device_count,
+    run, prun, resume, reset, srand, drawn_key, device_count,
 )
 from .seqmc import SeqMC, SeqMCChain, run_seqmc, resume_seqmc  # noqa: F401
 from . import stats  # noqa: F401

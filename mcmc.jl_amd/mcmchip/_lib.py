@@ -53,7 +53,8 @@ EXPORTED_SYMBOLS = (
     "mcmc_chains_create", "mcmc_chains_destroy", "mcmc_chains_reset", "mcmc_chains_set_state", "mcmc_chains_fork",
     "mcmc_chains_steps_done", "mcmc_chains_evals",
     "mcmc_chains_ram_factor", "mcmc_chains_tuner_state",
-    "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients", "mcmc_chains_reserve_outputs",
+    "mcmc_chains_set_steps_per_launch", "mcmc_chains_set_store_gradients", "mcmc_chains_set_tuner_burnin",
+    "mcmc_chains_reserve_outputs",
     "mcmc_chains_launches", "mcmc_chains_step_kernel", "mcmc_chains_store_leaps", "mcmc_run_serialmc",
     "mcmc_group_create", "mcmc_group_destroy", "mcmc_group_size", "mcmc_group_plan", "mcmc_group_chains_create",
     "mcmc_group_chains_destroy", "mcmc_group_chains_reset", "mcmc_group_chains_steps_done",
@@ -157,6 +158,7 @@ def load() -> ct.CDLL:
         "mcmc_chains_tuner_state": (ct.c_int, [P, ct.c_void_p, ct.c_void_p, ct.c_void_p]),
         "mcmc_chains_set_steps_per_launch": (ct.c_int, [P, i64]),
         "mcmc_chains_set_store_gradients": (ct.c_int, [P, i32]),
+        "mcmc_chains_set_tuner_burnin": (ct.c_int, [P, i64]),
         "mcmc_chains_reserve_outputs": (ct.c_int, [P, i64, i32]),
         "mcmc_chains_launches": (ct.c_int, [P, i64, ct.POINTER(i64)]),
         "mcmc_chains_step_kernel": (ct.c_int, [P, ct.c_char_p, i64]),

@@ -514,9 +514,21 @@ class _GlobalStream:
     own (MCMC.jl:87-98, SerialMC.jl:93-97).  Here a chain's stream is the Philox key (seed) and its global chain id
     (DESIGN.md §3), so the mirror of that global RNG is a seed plus a cursor over chain ids: a task spun by `*` (or
     resume) takes the next ids when it first runs, exactly as a Julia task first consumes the global RNG when it
-    runs.  srand(seed) restarts the cursor (Julia's srand)."""
+    runs.  srand(seed) restarts the cursor (Julia's srand).
+
+    The Philox key of a drawn stream is drawn_key(seed): the seed with the top bit set.  Explicit seeds (MCMCTask's
+    default seed=1, run(..., seed=s), SeqMC's target keys) live below 2^63, so a drawn chain never replays a chain a
+    task with an explicit seed and offset samples, whatever the two cursors are."""
     seed = 1
     next_chain = 0
+
+
+DRAWN_KEY_BIT = 1 << 63
+
+
+def drawn_key(seed: int) -> int:
+    """The Philox key of the global stream's chains under srand(seed): a key space of its own (top bit set)."""
+    return (int(seed) & (DRAWN_KEY_BIT - 1)) | DRAWN_KEY_BIT
 
 
 def srand(seed: int) -> None:
@@ -534,7 +546,7 @@ def _draw_chains(n: int):
         _GlobalStream.next_chain = 0
     first = _GlobalStream.next_chain
     _GlobalStream.next_chain += n
-    return _GlobalStream.seed, first
+    return drawn_key(_GlobalStream.seed), first
 
 
 def _spin(m, s, r):
@@ -595,7 +607,7 @@ class MCMCTask:
         if seed is None:
             seed = self.seed
             if seed is None and off is not None:
-                seed = _GlobalStream.seed
+                seed = drawn_key(_GlobalStream.seed)
         return MCMCTask(self.model, self.sampler, self.runner, nchains=nchains, seed=seed,
                         device=kw.get("device", self.device), chain_offset=off, init_x=kw.get("init_x"),
                         steps_per_launch=kw.get("steps_per_launch", self.steps_per_launch),
@@ -930,7 +942,7 @@ def prun(t, devices: Optional[Sequence[int]] = None):
         raise AssertionError("Runners do not have the same runner type")
     if not isinstance(t[-1].runner, SerialMC):
         return None                                          # the reference's prun only runs SerialMC tasks
-    if devices is None:
+    if devices is None and not getattr(t[0].sampler, "storeLeaps", False):   # storeLeaps records: one device
         nd = device_count()
         devices = tuple(range(nd)) if nd > 1 else None
     if all(_same_task_kind(x, t[0]) for x in t):
@@ -951,7 +963,7 @@ def resume(c, steps: int = 100, seed: Optional[int] = None, chain_offset: Option
     if seed is not None and chain_offset is None:
         chain_offset = 0
     if seed is None and chain_offset is not None:
-        seed = _GlobalStream.seed
+        seed = drawn_key(_GlobalStream.seed)
     nt = MCMCTask(t.model, t.sampler, SerialMC(steps=steps, thinning=t.runner.thinning), nchains=t.nchains,
                   seed=seed, device=t.device, chain_offset=chain_offset, init_x=t.init_x,
                   steps_per_launch=t.steps_per_launch, devices=t.devices)

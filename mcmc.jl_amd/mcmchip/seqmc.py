@@ -40,8 +40,8 @@ class _SeqCfg(ct.Structure):
 
 def target_seed(seed: int, t: int) -> int:
     """Philox key of target t's chains: distinct per target, so that particle n does not reuse the
-    same normals in every target of an outer step."""
-    return (int(seed) + (t + 1) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    same normals in every target of an outer step; below 2^63, the explicit-seed key space (api.drawn_key)."""
+    return (int(seed) + (t + 1) * 0x9E3779B97F4A7C15) & 0x7FFFFFFFFFFFFFFF
 
 
 class SeqMCChain(MCMCChain):

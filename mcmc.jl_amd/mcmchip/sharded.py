@@ -67,15 +67,18 @@ def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None,
     parts: name -> torch tensor [..., count] (accept bits: [..., ceil(count/64)] words), on the rank's GPU
     (NCCL) or on the host (gloo).  Rank r's columns are the global chains shard(nchains, world, r).  The
     transfer is point to point in chunks (runs of whole leading rows, e.g. kept steps, of at most `chunk_bytes`)
-    and concurrent across sources: dst keeps up to `slots` receives in flight from EVERY source rank at once, each
-    into its own buffer, and as a receive lands its chunk goes on to host memory (NCCL: an asynchronous device ->
-    page-locked host copy on a side stream, so the next receive into the other buffer overlaps it) and is then
-    placed into the destination array.  So `dst` holds at most `slots` chunks per source on its device (the world's
-    outputs are never concatenated on one GPU: at the 8-GPU metric they would be 193 GB).  Returns name -> numpy
-    array over all `nchains` chains (bits: ceil(nchains/64) words) on dst, None elsewhere.  `stats` (a dict, dst
-    only) receives `bytes` (received from other ranks), `max_recv_buffer_bytes` (the largest one buffer),
-    `max_buffer_bytes_per_source`, `max_sources_in_flight` (source ranks with a receive outstanding at one time)
-    and `max_chunks_in_flight`."""
+    and concurrent across sources, in rounds: round k moves chunk k of every source that has one, and its receives
+    on dst (one per source) are posted together as ONE dist.batch_isend_irecv -- one NCCL group call on the process
+    group's communicator, so no two p2p communicators of one device ever have operations outstanding at once; each
+    source posts its send of round k the same way.  `slots` rounds are in flight at a time, each into its own buffer
+    per source; as a round lands its chunks go on to host memory (NCCL: an asynchronous device -> page-locked host
+    copy on a side stream, so the next round's receives overlap it) and are then placed into the destination
+    arrays.  So `dst` holds at most `slots` chunks per source on its device (the world's outputs are never
+    concatenated on one GPU: at the 8-GPU metric they would be 193 GB).  Returns name -> numpy array over all
+    `nchains` chains (bits: ceil(nchains/64) words) on dst, None elsewhere.  `stats` (a dict, dst only) receives
+    `bytes` (received from other ranks), `max_recv_buffer_bytes` (the largest one buffer),
+    `max_buffer_bytes_per_source`, `max_sources_in_flight` (source ranks with a receive outstanding at one time),
+    `max_chunks_in_flight`, `rounds` and `group_calls` (batch_isend_irecv calls on dst)."""
     import collections
     import torch
     import torch.distributed as dist
@@ -102,18 +105,20 @@ def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None,
             width = (cnt + 63) // 64 if is_bits else cnt
             per = max(1, chunk_bytes // max(1, width * parts[n].element_size()))
             plans[r].append(_Plan(n, rowsof[n], width, off // 64 if is_bits else off, per))
-    out = None
     if rank != dst:
-        # the sender: every chunk of every array in plan order, at most `slots` sends outstanding
-        works = collections.deque()
+        # the source: chunk k is its send of round k, one batch_isend_irecv each, at most `slots` rounds outstanding
+        pending = collections.deque()
         for pl in plans[rank]:
             mine = parts[pl.name].reshape(pl.rows, parts[pl.name].shape[-1])[:, :pl.width]
             for r0, n in pl.chunks:
-                while len(works) >= slots:
-                    works.popleft().wait()
-                works.append(dist.isend(mine[r0:r0 + n].contiguous(), dst=glob(dst), group=group))
-        while works:
-            works.popleft().wait()
+                while len(pending) >= slots:
+                    for w in pending.popleft()[0]:
+                        w.wait()
+                t = mine[r0:r0 + n].contiguous()
+                pending.append((dist.batch_isend_irecv([dist.P2POp(dist.isend, t, glob(dst), group)]), t))
+        while pending:
+            for w in pending.popleft()[0]:
+                w.wait()
         return None
     # dst: host arrays, its own columns copied directly
     host = {}
@@ -124,19 +129,18 @@ def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None,
     for pl in plans[dst]:
         mine = parts[pl.name].reshape(pl.rows, parts[pl.name].shape[-1])[:, :pl.width]
         host[pl.name][:, pl.woff:pl.woff + pl.width] = mine.cpu().numpy()
-    queues = {r: collections.deque((pl, r0, n) for pl in plans[r] for r0, n in pl.chunks)
-              for r in range(world) if r != dst and plans[r]}
+    chunks = {r: [(pl, r0, n) for pl in plans[r] for r0, n in pl.chunks] for r in range(world) if r != dst and plans[r]}
+    rounds = max((len(v) for v in chunks.values()), default=0)
     dev = next(iter(parts.values())).device
     esz = {n: parts[n].element_size() for n in names}
     dtype = {n: parts[n].dtype for n in names}
     side = torch.cuda.Stream(device=dev) if on_gpu else None
     bufs = {}                                             # (source, slot) -> device (or host) buffer, reused
     stage = {}                                            # (source, slot) -> page-locked host staging (NCCL)
-    free = {r: collections.deque(range(slots)) for r in queues}
-    flight = collections.deque()                          # (source, slot, plan, row0, nrows, work) in post order
-    copying = collections.deque()                         # (source, slot, plan, row0, nrows, event): D2H under way
+    inflight = collections.deque()                        # (round, [(source, slot, plan, row0, nrows, view)], works)
+    copying = collections.deque()                         # (round, source, slot, plan, row0, nrows, event)
     max_buf = max_src_buf = moved = 0
-    max_src = max_chunks = 0
+    max_src = max_chunks = calls = 0
     src_buf_bytes = collections.Counter()
 
     def buffer(key, pl, n):
@@ -157,33 +161,24 @@ def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None,
     def place(pl, r0, n, arr):
         host[pl.name][r0:r0 + n, pl.woff:pl.woff + pl.width] = arr
 
-    def finish_copies(block_all):
-        while copying and (block_all or copying[0][5].query()):
-            r, k, pl, r0, n, ev = copying.popleft()
+    def finish_copies(upto):
+        # copies of rounds <= upto to their place (their staging buffers are reused by round upto + slots)
+        while copying and copying[0][0] <= upto:
+            _, r, k, pl, r0, n, ev = copying.popleft()
             ev.synchronize()
             st = stage[(r, k)][:n * pl.width * esz[pl.name]].view(dtype[pl.name]).view(n, pl.width)
             place(pl, r0, n, st.numpy())
-            free[r].append(k)
 
-    t0 = time.perf_counter()
-    while queues or flight or copying:
-        # post: every source with a chunk left and a free buffer
-        for r in list(queues):
-            while queues[r] and free[r]:
-                pl, r0, n = queues[r].popleft()
-                k = free[r].popleft()
-                view = buffer((r, k), pl, n)
-                flight.append((r, k, pl, r0, n, view, dist.irecv(view, src=glob(r), group=group)))
-            if not queues[r]:
-                del queues[r]
-        max_chunks = max(max_chunks, len(flight))
-        max_src = max(max_src, len({f[0] for f in flight}))
-        if flight:
-            r, k, pl, r0, n, view, work = flight.popleft()
-            work.wait()
+    def complete(rnd, entries, works):
+        nonlocal moved
+        for w in works:
+            w.wait()
+        finish_copies(rnd - slots)
+        if on_gpu:
+            side.wait_stream(torch.cuda.current_stream(dev))
+        for r, k, pl, r0, n, view in entries:
             moved += n * pl.width * esz[pl.name]
             if on_gpu:
-                side.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(side):
                     st = stage[(r, k)][:n * pl.width * esz[pl.name]].view(dtype[pl.name]).view(n, pl.width)
                     st.copy_(view, non_blocking=True)
@@ -192,19 +187,35 @@ def gather_shards(parts: dict, count: int, block: int, nchains: int, group=None,
                 # the next receive into this buffer runs on the NCCL stream after the current stream: make the
                 # current stream wait for the copy out of it
                 torch.cuda.current_stream(dev).wait_event(ev)
-                copying.append((r, k, pl, r0, n, ev))
-                finish_copies(False)
+                copying.append((rnd, r, k, pl, r0, n, ev))
             else:
                 place(pl, r0, n, view.numpy())
-                free[r].append(k)
-        else:
-            finish_copies(True)
+
+    t0 = time.perf_counter()
+    for k in range(rounds):
+        slot = k % slots
+        while inflight and inflight[0][0] <= k - slots:        # slot's previous round landed before its reuse
+            complete(*inflight.popleft())
+        ops, entries = [], []
+        for r, lst in chunks.items():
+            if k < len(lst):
+                pl, r0, n = lst[k]
+                view = buffer((r, slot), pl, n)
+                ops.append(dist.P2POp(dist.irecv, view, glob(r), group))
+                entries.append((r, slot, pl, r0, n, view))
+        inflight.append((k, entries, dist.batch_isend_irecv(ops)))
+        calls += 1
+        max_chunks = max(max_chunks, sum(len(e) for _, e, _ in inflight))
+        max_src = max(max_src, len({e[0] for _, es, _ in inflight for e in es}))
+    while inflight:
+        complete(*inflight.popleft())
+    finish_copies(rounds)
     out = {n: host[n].reshape(lead[n] + (host[n].shape[1],)) for n in names}
     if stats is not None:
         sec = time.perf_counter() - t0
         stats.update(bytes=moved, max_recv_buffer_bytes=max_buf, max_buffer_bytes_per_source=max_src_buf,
                      max_sources_in_flight=max_src, max_chunks_in_flight=max_chunks, slots=slots, seconds=sec,
-                     GB_per_s=moved / sec / 1e9 if sec > 0 else None)
+                     rounds=rounds, group_calls=calls, GB_per_s=moved / sec / 1e9 if sec > 0 else None)
     return out
 
 

@@ -290,7 +290,8 @@ def test_julia_hook_defines_batched_runners_reset_ou_and_leaps():
     fixed seed."""
     jl = open(os.path.join(ROOT, "mcmc.jl_amd", "julia", "mcmc_jl_hook.jl")).read()
     for needle in ("function run(t::Array{MCMCTask}; args...)", "function prun(t::Array{MCMCTask}; args...)",
-                   "hip_batchable(t) && return hip_run_tasks(t, false)", "hip_batchable(t) && return hip_run_tasks(t, true)",
+                   "hip_batchable(t) && return hip_run_tasks(t, false)",
+                   "hip_batchable(t) && return hip_run_tasks(t, true, hip_devices())",
                    "run_seqmc(t; args...)", "pmap(run_serialmc_exit, t)", "run_serialtempmc(t)",
                    "task_local_storage(:reset,", ":ou => 9", "mcmc_chains_fork", "mcmc_chains_set_state",
                    'diag["leaps"] = hip_leap_states', 'diags["leaps"]', "HMCSample(", "mcmc_chains_store_leaps",
@@ -300,6 +301,35 @@ def test_julia_hook_defines_batched_runners_reset_ou_and_leaps():
     plain = open(os.path.join(ROOT, "mcmc.jl_amd", "julia", "MCMCHip.jl")).read()
     for needle in ("function ou_model", "MODEL_OU", "mcmc_chains_set_state", "mcmc_chains_fork"):
         assert needle in plain, needle
+
+
+def test_julia_hook_runner_semantics():
+    """The hook's runner semantics, as text (no Julia here; tests/test_hook_protocol.py drives the
+    same C calls on the GPU): every task sets its runner's burnin as the tuners' burnin on its chains (fresh and
+    forked), chunks are at most the task runner's len, the tasks of one model share one uploaded model, prun of like
+    GPU tasks runs one mcmc_group over every visible device, SeqMC arrays of GPU targets go to mcmc_run_seqmc, drawn
+    streams use their own key space, and the ESS of a GPU batch is one mcmc_stats_ess call."""
+    import re
+    jl = open(os.path.join(ROOT, "mcmc.jl_amd", "julia", "mcmc_jl_hook.jl")).read()
+    ens = jl[jl.index("function hip_ensure!"):jl.index("end", jl.index("hip_set_tuner_burnin!(st.chains"))]
+    assert ens.index("HipChains(st.src, st.first, 1)") < ens.index("hip_set_tuner_burnin!(st.chains, "
+                                                                     "hip_tuner_burnin(st.runner))")
+    assert "hip_tuner_burnin(r::MCMCRunner) = (isa(r, SerialMC) || isa(r, SeqMC)) ? r.burnin : 0" in jl
+    assert "ccall((:mcmc_chains_set_tuner_burnin, hiplib), Cint, (Ptr{Void}, Int64)" in jl
+    assert "n = isa(st.runner, SerialMC) ? min(hip_chunk, st.runner.len) : 1" in jl
+    assert "HipTaskState(m, s, r)" in jl and "HipModelHandle(hip_context(m.device), m)" in jl
+    assert jl.count("HipModelHandle(") == 2            # its inner constructor and the one cached construction
+    assert "hip_batchable(t) && return hip_run_tasks(t, true, hip_devices())" in jl
+    for sym in ("mcmc_group_create", "mcmc_group_chains_create", "mcmc_group_run_serialmc",
+                "mcmc_group_chains_destroy", "mcmc_device_count", "mcmc_run_seqmc", "mcmc_stats_ess"):
+        assert f"ccall((:{sym}, hiplib)" in jl, sym
+    assert "isa(lastrunner, SeqMC) && hip_seqmc_able(t) && return hip_run_seqmc(t; args...)" in jl
+    assert "function ess(cs::Array{MCMCChain}" in jl
+    assert "hip_key(seed::Int) = (uint64(seed) & 0x7fffffffffffffff) | 0x8000000000000000" in jl
+    # every library function the hook calls is declared in the header
+    hdr = open(os.path.join(ROOT, "include", "mcmc_hip.h")).read()
+    for sym in set(re.findall(r"ccall\(\(:(\w+), hiplib\)", jl)):
+        assert re.search(r"\b" + sym + r"\(", hdr), sym
 
 
 def test_spun_tasks_draw_from_the_global_stream():
@@ -315,15 +345,34 @@ def test_spun_tasks_draw_from_the_global_stream():
     assert not api._same_task_kind((m * mc.MALA(0.1) * r), ts[0])
     assert not api._same_task_kind((m * mc.RWM(0.2) * r), ts[0])
     mc.srand(5)
-    assert api._draw_chains(3) == (5, 0) and api._draw_chains(2) == (5, 3)
+    assert api._draw_chains(3) == (api.drawn_key(5), 0) and api._draw_chains(2) == (api.drawn_key(5), 3)
     api._GlobalStream.next_chain = (1 << 32) - 1
-    assert api._draw_chains(2) == (6, 0)
+    assert api._draw_chains(2) == (api.drawn_key(6), 0)
     mc.srand(9)
     b = t.batch(64)
     assert b.seed is None and b.chain_offset is None
     b._draw()
-    assert (b.seed, b.chain_offset) == (9, 0) and api._GlobalStream.next_chain == 64
+    assert (b.seed, b.chain_offset) == (api.drawn_key(9), 0) and api._GlobalStream.next_chain == 64
     e = t.batch(64, seed=3)
     assert (e.seed, e.chain_offset) == (3, 0)
     with pytest.raises(ValueError):
         mc.MCMCTask(m, mc.RWM(0.1), r, seed=None, chain_offset=4)
+    # drawn streams have their own key space: no explicit seed (< 2^63) names a drawn stream
+    assert api.drawn_key(1) == (1 << 63) | 1 and api.drawn_key(1) != 1 and api.drawn_key(api.drawn_key(3)) == api.drawn_key(3)
+    from mcmchip.seqmc import target_seed
+    assert all(target_seed(s, k) < 1 << 63 for s in (1, 2**63 - 1, 12345) for k in range(5))
+
+
+def test_prun_dispatch_devices(monkeypatch):
+    """prun of like tasks: one group over every visible GPU, except storeLeaps samplers, whose records are built for
+    one device (host logic only: the batch runner is stubbed)."""
+    from mcmchip import api
+    seen = []
+    monkeypatch.setattr(api, "device_count", lambda: 4)
+    monkeypatch.setattr(api, "_run_batched", lambda ts, stop=False, devices=None: seen.append((stop, devices)) or [])
+    m = mc.model(mc.IsoNormalDot(), init=np.ones(3), grad=True)
+    r = mc.SerialMC(steps=10)
+    mc.prun(m * [mc.HMC(3, 0.1), mc.HMC(3, 0.1)] * r)
+    mc.prun(m * [mc.HMC(3, 0.1, storeLeaps=True), mc.HMC(3, 0.1, storeLeaps=True)] * r)
+    mc.prun(m * [mc.RWM(0.1)] * r, devices=(1, 2))
+    assert seen == [(True, (0, 1, 2, 3)), (True, None), (True, (1, 2))]

@@ -78,7 +78,8 @@ def _worker(rank, world, port, total, nk, d, q, chunk=None, slots=2):
 def test_gather_shards_gloo(world, total, chunk):
     """The chunked point-to-point gather reassembles every array exactly, whatever the chunk size (64 B: one
     row per message); every receive buffer holds at most one chunk (one row when a row is larger than the chunk),
-    at most two per source rank, and with several source ranks their receives are in flight together."""
+    at most two per source rank, and with several source ranks their receives are in flight together, posted as one
+    batch_isend_irecv group per round (the RCCL N > 1 path itself is unmeasured until the driver's 8-GPU run)."""
     nk, d = 3, 2
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
@@ -106,3 +107,6 @@ def test_gather_shards_gloo(world, total, chunk):
     if sum(c > 0 for c in cnts) >= 2:
         assert st["max_sources_in_flight"] >= 2             # receives from several ranks outstanding together
     assert st["GB_per_s"] > 0
+    # one batch_isend_irecv (one RCCL group call) per round on dst, the round's receives from every source in it
+    assert st["group_calls"] == st["rounds"] >= 1
+    assert st["max_chunks_in_flight"] <= 2 * sum(c > 0 for c in cnts)

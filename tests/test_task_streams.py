@@ -31,7 +31,7 @@ def test_array_of_tasks_gives_independent_chains(gpu):
     ts = m * [mc.RWM(0.1), mc.RWM(0.1)] * r
     chs = mc.run(ts)
     assert len(chs) == 2 and chs[0].task is ts[0] and chs[1].task is ts[1]
-    assert ts[0].seed == ts[1].seed == 1 and ts[1].chain_offset == ts[0].chain_offset + 1
+    assert ts[0].seed == ts[1].seed == mc.drawn_key(1) and ts[1].chain_offset == ts[0].chain_offset + 1
     assert not np.array_equal(chs[0]._samples, chs[1]._samples)
     for t, ch in zip(ts, chs):
         _, (s, g, acc) = _oracle_chain(m, mc.RWM(0.1), t, r)
@@ -46,11 +46,28 @@ def test_respun_tasks_draw_new_streams(gpu):
     r = mc.SerialMC(steps=50)
     a = mc.run(m * mc.RWM(0.3) * r)
     b = mc.run(m * mc.RWM(0.3) * r)
-    assert (a.task.seed, a.task.chain_offset) == (7, 0) and (b.task.seed, b.task.chain_offset) == (7, 1)
+    assert (a.task.seed, a.task.chain_offset) == (mc.drawn_key(7), 0)
+    assert (b.task.seed, b.task.chain_offset) == (mc.drawn_key(7), 1)
     assert not np.array_equal(a._samples, b._samples)
     mc.srand(7)
     c = mc.run(m * mc.RWM(0.3) * r)                     # srand restarts the stream
     assert np.array_equal(a._samples, c._samples)
+
+
+def test_explicit_seed_and_drawn_streams_do_not_overlap(gpu):
+    """MCMCTask(m, s, r, nchains=4) (seed 1, chain ids 0..3) and a later run(m * s * r) under srand(1) (the global
+    stream's ids 0, 1, ...) sample different chains: drawn keys have their own key space."""
+    mc.srand(1)
+    m = _model("iso", 3)
+    r = mc.SerialMC(steps=60)
+    a = mc.run(mc.MCMCTask(m, mc.RWM(0.3), r, nchains=4))
+    b = mc.run(m * mc.RWM(0.3) * r)
+    assert (b.task.seed, b.task.chain_offset) == (mc.drawn_key(1), 0)
+    assert not np.array_equal(a._samples[:, :, 0], b._samples[:, :, 0])
+    c = mc.resume(a, steps=60)                           # a new task from model.init on the drawn stream
+    assert not any(np.array_equal(c._samples[:, :, k], a._samples[:, :, k]) for k in range(4))
+    _, (s, g, acc) = _oracle_chain(m, mc.RWM(0.3), b.task, r)
+    assert_parity(b, s, g, acc, "rwm")
 
 
 SAMPLERS = {
