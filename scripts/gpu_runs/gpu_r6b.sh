@@ -5,6 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r6b
 mkdir -p $O
 run() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name exit $rc"; [ $rc -eq 0 ] || exit $rc; }
+run gputests 600 python3 -u -m pytest tests/test_hook_protocol.py tests/test_task_streams.py tests/test_seqmc.py tests/test_sharded_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 export PMC_GROUPS="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CU_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE"
 run pmc_bare_normal 300 bash scripts/gpu_pmc.sh r6b_bare_normal --config bare_normal --no-ess
 run pmc_mala32 300 bash scripts/gpu_pmc.sh r6b_mala32 --sampler mala --no-ess
