@@ -699,7 +699,7 @@ def main():
                                 "fused kernel never moves them, so this rate can exceed HBM peak: it is the north "
                                 "star's '% of HBM roofline' yardstick, not a roofline"}
         vm = measured_valu(kname, wkey)
-        if vm is not None:
+        if vm is not None and args.sampler != "ram":
             # the binding resource: VALU issue.  SQ_ACTIVE_INST_VALU quad-cycles x 4 = SIMD-cycles of VALU issue
             # per chain-step (measured, committed profile of this kernel instance); achieved = that x chain-steps
             # per launch / the live launch time; peak = 1024 SIMDs x 2.4 GHz (the spec engine clock)
@@ -727,6 +727,12 @@ def main():
                              if args.sampler == "ram" else
                              "no committed VALU profile of this kernel instance built from these sources "
                              "(profiles/valu.json src_hash): HBM roofline of the fused design")}
+        if args.sampler == "ram" and vm is not None:
+            # RAM binds on HBM (the factor); the profile's VALU issue rides along
+            cyc = 4.0 * vm["valu_quadcycles_per_chain_step"]
+            roof["valu"] = {"achieved": cyc * units / avg_launch_s / 1e12, "peak": VALU_PEAK_TCYC,
+                            "unit": "T VALU-issue-cycles/s", "frac": cyc * units / avg_launch_s / 1e12 / VALU_PEAK_TCYC,
+                            "valu_busy_measured": vm["valu_busy"], "source": vm["source"]}
         if C <= 64:
             roof["binding"] = ("latency: a few-chain kernel runs each chain's steps as one dependent chain of "
                                "operations (C <= 64: lpc_rwm_spec / lpc_rwm_la), so neither the VALU nor the HBM "
@@ -741,6 +747,26 @@ def main():
                 "evals_per_launch": evals / launches,
                 "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
                         "device); 4 n d fp64 flop each (SURVEY.md §8(d))"}
+        if args.sampler == "ram":
+            # RAM on a regression target: the jump factor S (d(d+1)/2 doubles a chain) is read and written every
+            # step (glm_ram, glm_ram_wave.hip), beside the state's round trip; HBM against the MFMA eval, the
+            # larger fraction names the bound
+            ram_b = C * K * (8.0 * d * (d + 1) + 16.0 * d + 16.0) + C * nkept * (8.0 * d + 1 / 8)
+            hbm_ach = ram_b / launches / avg_launch_s / 1e9
+            hbm = {"achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_ach / HBM_PEAK_GBS,
+                   "algorithmic_bytes_per_launch": ram_b / launches, "traffic": traffic,
+                   "bytes_per_unit": {"chain_step": 8.0 * d * (d + 1) + 16.0 * d + 16.0, "kept_chain_step": 8.0 * d},
+                   "note": "the RAM jump factor read and written every step + the state round trip + kept rows"}
+            if hbm["frac"] >= roof["frac"]:
+                mf = dict(roof)
+                for k in ("kernel", "launches", "avg_launch_ms", "traffic", "traffic_detail"):
+                    mf.pop(k, None)
+                roof = {"bound": "hbm", "achieved": hbm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": hbm["frac"], "traffic": traffic, "kernel": kname, "launches": launches,
+                        "avg_launch_ms": avg_launch_s * 1e3, "algorithmic_bytes_per_launch": ram_b / launches,
+                        "bytes_per_unit": hbm["bytes_per_unit"], "mfma": mf, "note": hbm["note"]}
+            else:
+                roof["hbm"] = hbm
         fm = measured_fp64(kname, wkey)
         if fm is not None:                                            # MFMA + VALU fp64 on the shared datapath
             per_eval = fm["mfma_flop_per_eval"] + fm["valu_fp64_flop_per_eval"]
