@@ -1210,8 +1210,42 @@ __host__ __device__ constexpr int glm_ws_region(int XS) {
 __host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
     const int XS = glm_tile_doubles(16 * nm);
     const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
-    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16);
+    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16)
+#ifdef GLM_WS_STAMP
+           + 512                                               // the phase stamps (dev build, scripts/ws_stamps.py)
+#endif
+        ;
 }
+#ifdef GLM_WS_STAMP
+// GLM_WS_STAMP (dev build only, scripts/ws_stamps.py): shader-clock stamps (low 32 bits) of glm_mala1ws's tile loop,
+// every wave of workgroups 0..3, tiles 8..23: M waves at the loop top, eta_{t+1} stored, G_{t-1} issued, past the
+// barrier; V waves at the loop top, tile t+2 stored / t+3 issued, the terms of tile t done, r_t stored, past the
+// barrier.  Kept in LDS past the kernel's own and copied out after the loop.
+static __device__ unsigned g_ws_stamps[4][8][16][8];
+static __device__ unsigned g_ws_wg[4][8][8];           // per wave: start, proposal, bx/tile 2, eta_0, loop end, final barrier, end
+static __device__ unsigned g_ws_wg2[4][8][4];          // inside the proposal phase (V: normals done, qf summed, table; M: tiles 0, 1)
+#define WS_WG2(pt)                                                                                     \
+    do {                                                                                               \
+        const unsigned ts_ = (unsigned)__builtin_amdgcn_s_memtime();                                  \
+        if (blockIdx.x < 4 && (threadIdx.x & 63) == 0) g_ws_wg2[blockIdx.x][threadIdx.x >> 6][pt] = ts_; \
+    } while (0)
+#define WS_WG(pt)                                                                                      \
+    do {                                                                                               \
+        const unsigned ts_ = (unsigned)__builtin_amdgcn_s_memtime();                                  \
+        if (blockIdx.x < 4 && (threadIdx.x & 63) == 0) g_ws_wg[blockIdx.x][threadIdx.x >> 6][pt] = ts_; \
+    } while (0)
+#define WS_STAMP(pt)                                                                                   \
+    do {                                                                                               \
+        if (t >= 8 && t < 24) {                                                                        \
+            const unsigned ts_ = (unsigned)__builtin_amdgcn_s_memtime();                              \
+            if (p.lane == 0) wst[(wv * 16 + (int)(t - 8)) * 8 + (pt)] = ts_;                          \
+        }                                                                                              \
+    } while (0)
+#else
+#define WS_STAMP(pt) do { } while (0)
+#define WS_WG(pt) do { } while (0)
+#define WS_WG2(pt) do { } while (0)
+#endif
 template <int NM>
 __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1246,6 +1280,9 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double* const ltabp = Yb + 64;                             // logistic term's table [SP_NROWS][10]
     double* const qfl = ltabp + SP_NROWS * 10;                 // qf [4][16], then lik [4][16]
     double* const likl = qfl + 64;
+#ifdef GLM_WS_STAMP
+    unsigned* const wst = reinterpret_cast<unsigned*>(likl + 64);
+#endif
     auto xslot = [&](int64_t tt) -> double* { const int b = (int)(tt & 3); return b < 2 ? Xs + b * XS : R + (b - 2) * XS; };
     const Stream rs{s.key0, s.key1};
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
@@ -1285,7 +1322,10 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double* const xb = beta + (size_t)(p.tile * NS) * 64 + p.lane;   // this lane's proposal slots
 
     // ---- proposal phase: V waves draw the proposal (MALA.jl:98-103) into LDS; M waves stage X tiles 0 and 1
+    WS_WG(0);
     if (vwave) {
+        // every state load unconditional (an invalid slot reads the lane's row 0 and is zeroed): no masked load
+        // and wait per slot, the loads of several slots in flight together
         double qf = 0.0;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
@@ -1298,9 +1338,10 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
             for (int e = 0; e < 4; ++e) {
                 const int slot = 4 * m + e;
                 const bool v = glm_valid(a, p, slot);
-                const size_t o = (size_t)(16 * m + e) * ld;
-                const double xv = v ? xl[o] : 0.0;
-                const double gv = v ? gl[o] : 0.0;
+                const size_t o = v ? (size_t)(16 * m + e) * ld : 0;
+                const double xl0 = xl[o], gl0 = gl[o];
+                const double xv = v ? xl0 : 0.0;
+                const double gv = v ? gl0 : 0.0;
                 const double pm = xv + half * gv;                               // MALA.jl:98
                 const double xpv = pm + sq * (v ? z[e] : 0.0);                  // MALA.jl:100
                 const double ee = pm - xpv;
@@ -1308,20 +1349,26 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                 xb[64 * slot] = xpv;
             }
         }
+        WS_WG2(0);
         qf = glm_sum(a, p, GlmLds{}, qf);
         if (p.q == 0) qfl[p.tile * 16 + p.cl] = qf;
+        WS_WG2(1);
         if (logi) {
             for (int e = u; e < SP_NROWS * 10; e += 256) ltabp[e] = (&kSoftplusTab[0][0])[e];
         }
+        WS_WG2(2);
     } else {
         load_tile(0);
         store_tile(0);
+        WS_WG2(0);
         if (ntiles > 1) {
             load_tile(1);
             store_tile(1);
         }
+        WS_WG2(1);
     }
     __syncthreads();
+    WS_WG(1);
     // ---- M: the proposal into registers, eta_0;  V: X tile 2 into registers (slot 2 overlays the proposal)
     double bx[NS];
     f64x4 G[NM];
@@ -1334,6 +1381,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         load_tile(2);
     }
     __syncthreads();                                           // the proposal area is free from here on
+    WS_WG(2);
     f64x4* const Eq = reinterpret_cast<f64x4*>(Eb) + p.tile * 64 + p.lane;   // + 256 * buffer
     f64x4* const Rq = reinterpret_cast<f64x4*>(Rb) + p.tile * 64 + p.lane;
     auto eta_of = [&](int64_t tt) {                            // glm_eval1_tiles' eta chain, operands read ahead
@@ -1373,6 +1421,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     };
     if (!vwave) Eq[0] = eta_of(0);
     __syncthreads();
+    WS_WG(3);
     // ---- the observation tiles
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = logi ? 0.0 : det_log(sn);
@@ -1385,16 +1434,22 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double ubnd = -__builtin_inf();                            // logistic: max of u + b over the lane's observations
     if (!vwave) {
         for (int64_t t = 0; t < ntiles; ++t) {
+            WS_STAMP(0);
             if (t + 1 < ntiles) Eq[256 * ((t + 1) & 1)] = eta_of(t + 1);
+            WS_STAMP(1);
             if (t >= 1) g_of(t - 1);
+            WS_STAMP(2);
             __syncthreads();
+            WS_STAMP(3);
         }
     } else {
         for (int64_t t = 0; t < ntiles; ++t) {
+            WS_STAMP(0);
             if (t + 2 < ntiles) {                              // slot (t+2) % 4 held tile t-2: read before the last barrier
                 store_tile(t + 2);
                 if (t + 3 < ntiles) load_tile(t + 3);
             }
+            WS_STAMP(1);
             const f64x4 eta = Eq[256 * (t & 1)];
             const double* LY = xslot(t) + YO;
             double y[4], term[4], rv[4];                       // y: the response, for the logistic model w (det_logi)
@@ -1441,10 +1496,18 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                     rv[r] = in ? rv[r] : 0.0;
                 }
             }
+            WS_STAMP(2);
             Rq[256 * (t & 1)] = f64x4{rv[0], rv[1], rv[2], rv[3]};
+            WS_STAMP(3);
             __syncthreads();
+            WS_STAMP(4);
         }
     }
+    WS_WG(4);
+#ifdef GLM_WS_STAMP
+    if (blockIdx.x < 4)
+        for (int j = p.lane; j < 128; j += 64) (&g_ws_stamps[blockIdx.x][wv][0][0])[j] = wst[wv * 128 + j];
+#endif
     if (vwave) {
         const double lik = glm_sum(a, p, GlmLds{}, logi && ubnd >= 0.0 ? -__builtin_inf() : lik_part);
         if (p.q == 0) likl[p.tile * 16 + p.cl] = lik;
@@ -1452,8 +1515,14 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         g_of(ntiles - 1);
     }
     __syncthreads();
+    WS_WG(5);
     if (vwave) return;
     // ---- M waves: the end of the evaluation (glm_finish), MALA.jl:104-125
+    // the current position (qb, and the kept rows of a rejected step), every load unconditional and issued first
+    double xo[NS];
+#pragma unroll
+    for (int slot = 0; slot < NS; ++slot)
+        xo[slot] = xl[glm_valid(a, p, slot) ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0];
     double lp = a.st.lp[cc];
     int32_t n_acc = sa.tuner ? a.st.t_acc[cc] : 0;
     int32_t n_prop = sa.tuner ? a.st.t_prop[cc] : 0;
@@ -1491,7 +1560,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
 #pragma unroll
     for (int slot = 0; slot < NS; ++slot) {
         const bool v = glm_valid(a, p, slot);
-        const double xv = v ? xl[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
+        const double xv = v ? xo[slot] : 0.0;
         const double e = (bx[slot] + half * G[slot >> 2][slot & 3]) - xv;           // MALA.jl:104-105
         if (v) qb = qb + ((-(e * e)) / twoh - Lc);
     }
@@ -1517,7 +1586,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                 xw[r * ld] = xv;
                 gw[r * ld] = gv;
             } else {
-                xv = xl[r * ld];
+                xv = xo[slot];
                 gv = gl[r * ld];
             }
             const size_t ko = (size_t)(4 * p.q + r) * Cs + (size_t)p.c;
@@ -1545,6 +1614,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         }
     }
     glm_count_evals(a, p, s.nsteps);
+    WS_WG(6);
 }
 
 // storeLeaps: leap l's state into the record, [l][d][C] and [l][C] (HMC.jl:145-150)
@@ -1734,6 +1804,17 @@ static unsigned glm_grid(int64_t C, const GlmShape& g) {
 }  // namespace mcmc
 
 #ifdef GLM_MALA1_UNIT
+#ifdef GLM_WS_STAMP
+extern "C" int mcmc_debug_ws_stamps(unsigned* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcmc::g_ws_stamps), sizeof(mcmc::g_ws_stamps)) == hipSuccess ? 0 : 4;
+}
+extern "C" int mcmc_debug_ws_wg(unsigned* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcmc::g_ws_wg), sizeof(mcmc::g_ws_wg)) == hipSuccess ? 0 : 4;
+}
+extern "C" int mcmc_debug_ws_wg2(unsigned* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcmc::g_ws_wg2), sizeof(mcmc::g_ws_wg2)) == hipSuccess ? 0 : 4;
+}
+#endif
 // glm_mala1.hip: the single-slice MALA kernels only, in a translation unit built with machine LICM
 hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
     using namespace mcmc;

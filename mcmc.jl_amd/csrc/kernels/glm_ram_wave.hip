@@ -6,31 +6,41 @@
 //   glm_ram_update  (every step)                the MH test (RAM.jl:62-71), the factor update (RAM.jl:74-78) with
 //                                               the next step's S rvec folded into it (ram_wave_update NEXT), and
 //                                               the next xprop
-// The factor is the wave-per-chain layout of ram_wave.hpp (one chain per wave, its rows over the 64 lanes); x stays
-// in the regression layout [d][ld] (the eval kernel's input), read and written per coordinate.  u (row layout) and
-// |rvec|^2 wait in HBM between the kernels.  Sums: the matvec and the update are ram_wave.hpp's, |rvec|^2 the
-// 64-lane wave order; oracle.c restates both (orc_chain, RAM on a regression target with d > 32).
+// The factor is the wave-per-chain layout of ram_wave.hpp: for 32 < d <= 256 two chains per wave, 32 lanes each (the
+// separable targets' HalfWaveChain: a column's pivot work is shared by two chains and no lane slot lies past d), for
+// d > 256 one chain per wave, its rows over the 64 lanes; x stays in the regression layout [d][ld] (the eval kernel's
+// input), read and written per coordinate.  u (row layout) and |rvec|^2 wait in HBM between the kernels.  Sums: the
+// matvec and the update are ram_wave.hpp's, |rvec|^2 the half-wave (d <= 256) or 64-lane wave order; oracle.c restates
+// both (orc_chain, RAM on a regression target with d > 32).
 #include "wpc_impl.hpp"
 #include "../ram_wave.hpp"
 
 namespace mcmc {
 
-// WaveChain's coordinate layout (lane l, slot 4 g + e <-> coordinate 4 (l + 64 g) + e) over the regression state
-// [d][ld] and the C ABI's kept layout [nkept][d][C]
-template <int G>
-struct GlmWaveChain : WaveChain<G, false, 1, kTabGlobal> {
-    using Base = WaveChain<G, false, 1, kTabGlobal>;
+// A wave-per-chain policy's coordinate layout (lane l of the chain's L, slot 4 g + e <-> coordinate 4 (l + L g) + e)
+// over the regression state [d][ld] and the C ABI's kept layout [nkept][d][C]; B = WaveChain (L = 64) or
+// HalfWaveChain (L = 32, two chains a wave)
+template <class B>
+struct GlmChain : B {
+    using Base = B;
     using Base::c;
     using Base::coord;
     using Base::live;
     using Base::valid;
     static constexpr int NC = Base::NC;
+    static constexpr int CPW = 64 / Base::L;                    // chains per wave
     int64_t ld;
-    __device__ explicit GlmWaveChain(const StepArgs& s) : Base(s) { ld = s.ld; }
+    __device__ explicit GlmChain(const StepArgs& s) : Base(s) { ld = s.ld; }
+    __device__ __forceinline__ int64_t cc() const { return live ? c : 0; }
+    // the wave's first chain (its factor block starts the buffer resource) and this lane's byte offset in it
+    __device__ __forceinline__ int64_t wave_chain0() const { return c - (int64_t)((threadIdx.x & 63) / Base::L); }
+    __device__ __forceinline__ uint32_t vo(int64_t ram_ld) const {
+        return (uint32_t)((threadIdx.x & 63) / Base::L) * (uint32_t)(ram_ld * 8) + (uint32_t)Base::lane * 8u;
+    }
     __device__ __forceinline__ void load_glm(const double* x, double (&v)[NC]) const {
-        const int64_t cc = live ? c : 0;
+        const int64_t c0 = cc();
 #pragma unroll
-        for (int k = 0; k < NC; ++k) v[k] = valid(k) ? x[(size_t)coord(k) * (size_t)ld + (size_t)cc] : 0.0;
+        for (int k = 0; k < NC; ++k) v[k] = valid(k) ? x[(size_t)coord(k) * (size_t)ld + (size_t)c0] : 0.0;
     }
     __device__ __forceinline__ void store_glm(double* x, const double (&v)[NC]) const {
         if (!live) return;
@@ -46,28 +56,36 @@ struct GlmWaveChain : WaveChain<G, false, 1, kTabGlobal> {
             if (valid(k)) p[(size_t)coord(k) * (size_t)s.C] = v[k];
     }
 };
+template <int G>
+using GlmWaveChain = GlmChain<WaveChain<G, false, 1, kTabGlobal>>;
+template <int G>
+using GlmHalfWaveChain = GlmChain<HalfWaveChain<G>>;
 
-// the per-chain buffers between the kernels: u = S rvec in row layout [C][64 NC] and |rvec|^2 [C]
+// the per-chain buffers between the kernels: u = S rvec in row layout [C][ustride] and |rvec|^2 [C]
 struct GlmRamBufs {
     double* u;
     double* nz;
     double* xprop;      // [d][ld]
     const double* lpp;  // [C]
+    int64_t ustride;    // doubles of u per chain (mcmc_glm_ram_wave_ustride)
 };
 
-template <int G>
-__device__ __forceinline__ uint32_t glm_ram_vo(const GlmWaveChain<G>& p) { return (uint32_t)p.lane * 8u; }
+// the wave's chains exist (a tail wave with none leaves; with two chains a wave one half may be past C: its loads
+// read chain 0 or its own allocated factor block, its stores are skipped)
+template <class P>
+__device__ __forceinline__ bool glm_ram_wave_live(const P& p, const StepArgs& s) {
+    return p.wave_chain0() < s.C;
+}
 
-// rvec of step i, |rvec|^2 (wave order), u = S_(i-1) rvec; xprop = x + u
-template <int G>
+// rvec of step i, |rvec|^2 (the chain's lane order), u = S_(i-1) rvec; xprop = x + u
+template <class P>
 __global__ __launch_bounds__(kBlock) void glm_ram_prop(KernelArgs a, GlmRamBufs b) {
-    using P = GlmWaveChain<G>;
-    constexpr int NC = P::NC, L = 64;
+    constexpr int NC = P::NC, L = P::L, CPW = P::CPW;
     const StepArgs& s = a.s;
     const P p(s);
-    if (!p.live) return;                                          // wave-uniform: one chain a wave
+    if (!glm_ram_wave_live(p, s)) return;                        // wave-uniform
     __shared__ double xpose[kBlock / 64][64 * NC];
-    double* const slice = xpose[threadIdx.x >> 6];
+    double* const slice = &xpose[threadIdx.x >> 6][((threadIdx.x & 63) / L) * L * NC];
     const Stream rs{s.key0, s.key1};
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
     const int d = s.d;
@@ -83,12 +101,14 @@ __global__ __launch_bounds__(kBlock) void glm_ram_prop(KernelArgs a, GlmRamBufs 
     const double nz = p.reduce(a2);
     ram_to_rows<NC, L>(slice, p.lane, z, zr);
     const int64_t ld = a.st.ram_ld;
-    double* const B0 = a.st.ram_L + (uint64_t)p.c * (uint64_t)ld;
-    const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * (uint64_t)a.st.ram_hs, ld * 8);
-    ram_wave_matvec<NC, L>(Ss, glm_ram_vo(p), p.lane, d, zr, u);  // S * rvec
+    double* const B0 = a.st.ram_L + (uint64_t)p.wave_chain0() * (uint64_t)ld;
+    const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * (uint64_t)a.st.ram_hs, ld * 8 * CPW);
+    ram_wave_matvec<NC, L>(Ss, p.vo(ld), p.lane, d, zr, u);       // S * rvec
+    if (p.live) {
 #pragma unroll
-    for (int sl = 0; sl < NC; ++sl) b.u[(size_t)p.c * (64 * NC) + (size_t)(p.lane + L * sl)] = u[sl];
-    if (p.lane == 0) b.nz[p.c] = nz;
+        for (int sl = 0; sl < NC; ++sl) b.u[(size_t)p.c * (size_t)b.ustride + (size_t)(p.lane + L * sl)] = u[sl];
+        if (p.lane == 0) b.nz[p.c] = nz;
+    }
     ram_to_quads<NC, L>(slice, p.lane, u, uq);
     p.load_glm(a.st.x, x);
 #pragma unroll
@@ -97,27 +117,27 @@ __global__ __launch_bounds__(kBlock) void glm_ram_prop(KernelArgs a, GlmRamBufs 
 }
 
 // step i: accept (RAM.jl:62-71), kept rows, the factor update (RAM.jl:74-78); NEXT: step i + 1's u, |rvec|^2, xprop
-template <int G, bool NEXT>
+template <class P, bool NEXT>
 __global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBufs b) {
-    using P = GlmWaveChain<G>;
-    constexpr int NC = P::NC, L = 64;
+    constexpr int NC = P::NC, L = P::L, CPW = P::CPW;
     const StepArgs& s = a.s;
     const SamplerArgs& sa = a.sa;
     const P p(s);
-    if (!p.live) return;
+    if (!glm_ram_wave_live(p, s)) return;                        // wave-uniform
     __shared__ double xpose[kBlock / 64][64 * NC];
-    double* const slice = xpose[threadIdx.x >> 6];
+    double* const slice = &xpose[threadIdx.x >> 6][((threadIdx.x & 63) / L) * L * NC];
     const Stream rs{s.key0, s.key1};
     const uint32_t chain = s.chain0 + (uint32_t)p.c;
     const int d = s.d;
     const int64_t i = s.step_begin;
     double x[NC], u[NC], uq[NC];
     p.load_glm(a.st.x, x);
-    double lp = a.st.lp[p.c];
-    const double lpp = b.lpp[p.c];
+    const int64_t c0 = p.cc();
+    double lp = a.st.lp[c0];
+    const double lpp = b.lpp[c0];
 #pragma unroll
-    for (int sl = 0; sl < NC; ++sl) u[sl] = b.u[(size_t)p.c * (64 * NC) + (size_t)(p.lane + L * sl)];
-    const double nz = b.nz[p.c];
+    for (int sl = 0; sl < NC; ++sl) u[sl] = b.u[(size_t)c0 * (size_t)b.ustride + (size_t)(p.lane + L * sl)];
+    const double nz = b.nz[c0];
     ram_to_quads<NC, L>(slice, p.lane, u, uq);
     const double ratio = lpp - lp;
     const bool acc = mh_accept_short_circuit(rs, chain, (uint32_t)i, ratio);
@@ -134,10 +154,10 @@ __global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBuf
     }
     const double alpha = ram_alpha(i, d, ratio, sa.rate);
     const int64_t ld = a.st.ram_ld;
-    double* const B0 = a.st.ram_L + (uint64_t)p.c * (uint64_t)ld;
+    double* const B0 = a.st.ram_L + (uint64_t)p.wave_chain0() * (uint64_t)ld;
     const uint64_t hs = (uint64_t)a.st.ram_hs;
-    const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld * 8);
-    const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, ld * 8);
+    const ram_rsrc_t Ss = ram_chain_rsrc(B0 + (uint64_t)((i - 1) & 1) * hs, ld * 8 * CPW);
+    const ram_rsrc_t Sd = ram_chain_rsrc(B0 + (uint64_t)(i & 1) * hs, ld * 8 * CPW);
     double zn[NC], znr[NC], un[NC];
     double a2 = 0.0;
     if (NEXT) {
@@ -149,14 +169,16 @@ __global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBuf
         }
         ram_to_rows<NC, L>(slice, p.lane, zn, znr);
     }
-    ram_wave_update<NC, L, NEXT>(Ss, Sd, glm_ram_vo(p), p.lane, d, alpha, nz, u, znr, un);
+    ram_wave_update<NC, L, NEXT>(Ss, Sd, p.vo(ld), p.lane, d, alpha, nz, u, znr, un);
     p.store_glm(a.st.x, x);
-    if (p.lane == 0) a.st.lp[p.c] = lp;
+    if (p.live && p.lane == 0) a.st.lp[p.c] = lp;
     if (NEXT) {
+        if (p.live) {
 #pragma unroll
-        for (int sl = 0; sl < NC; ++sl) b.u[(size_t)p.c * (64 * NC) + (size_t)(p.lane + L * sl)] = un[sl];
+            for (int sl = 0; sl < NC; ++sl) b.u[(size_t)p.c * (size_t)b.ustride + (size_t)(p.lane + L * sl)] = un[sl];
+        }
         const double nzn = p.reduce(a2);
-        if (p.lane == 0) b.nz[p.c] = nzn;
+        if (p.live && p.lane == 0) b.nz[p.c] = nzn;
         ram_to_quads<NC, L>(slice, p.lane, un, uq);
 #pragma unroll
         for (int k = 0; k < NC; ++k) x[k] = x[k] + uq[k];
@@ -164,21 +186,22 @@ __global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBuf
     }
 }
 
-template <int G>
+template <class P>
 static hipError_t glm_ram_wave_g(const KernelArgs& a0, const GlmRamBufs& b0, double* lpp, hipStream_t st) {
-    const dim3 grid((unsigned)((a0.s.C + kChainsPerBlock - 1) / kChainsPerBlock));
+    const int64_t cpb = (int64_t)kChainsPerBlock * P::CPW;     // chains per 256-thread block
+    const dim3 grid((unsigned)((a0.s.C + cpb - 1) / cpb));
     KernelArgs a = a0;
     GlmRamBufs b = b0;
     b.lpp = lpp;
     a.s.nsteps = 1;
-    glm_ram_prop<G><<<grid, kBlock, 0, st>>>(a, b);
+    glm_ram_prop<P><<<grid, kBlock, 0, st>>>(a, b);
     hipError_t e = hipGetLastError();
     for (int t = 0; t < a0.s.nsteps && e == hipSuccess; ++t) {
         a.s.step_begin = a0.s.step_begin + t;
         e = mcmc_launch_glm_eval(a, b.xprop, lpp, nullptr, 0, st);           // the log-target at xprop
         if (e != hipSuccess) break;
-        if (t + 1 < a0.s.nsteps) glm_ram_update<G, true><<<grid, kBlock, 0, st>>>(a, b);
-        else glm_ram_update<G, false><<<grid, kBlock, 0, st>>>(a, b);
+        if (t + 1 < a0.s.nsteps) glm_ram_update<P, true><<<grid, kBlock, 0, st>>>(a, b);
+        else glm_ram_update<P, false><<<grid, kBlock, 0, st>>>(a, b);
         e = hipGetLastError();
     }
     return e;
@@ -192,13 +215,18 @@ int64_t mcmc_glm_ram_wave_ustride(int d) { return d <= 256 ? 256 : d <= 512 ? 51
 hipError_t mcmc_launch_glm_ram_wave(const mcmc::KernelArgs& a, double* u, double* nz, double* xprop, double* lpp,
                                     hipStream_t st) {
     using namespace mcmc;
-    const GlmRamBufs b{u, nz, xprop, nullptr};
+    const GlmRamBufs b{u, nz, xprop, nullptr, mcmc_glm_ram_wave_ustride(a.s.d)};
+    if (a.s.d <= 256) {                                       // two chains a wave (32 lanes each, 128 G rows)
+        const int g = a.s.d <= 128 ? 1 : 2;
+        mcmc_note_step_kernel("glm_ram_update<GlmHalfWaveChain<%d>, true>", g);
+        return g == 1 ? glm_ram_wave_g<GlmHalfWaveChain<1>>(a, b, lpp, st)
+                      : glm_ram_wave_g<GlmHalfWaveChain<2>>(a, b, lpp, st);
+    }
     const int g = wpc_nb_for(a.s.d);
-    mcmc_note_step_kernel("glm_ram_update<%d, true>", g);
+    mcmc_note_step_kernel("glm_ram_update<GlmWaveChain<%d>, true>", g);
     switch (g) {
-        case 1: return glm_ram_wave_g<1>(a, b, lpp, st);
-        case 2: return glm_ram_wave_g<2>(a, b, lpp, st);
-        case 4: return glm_ram_wave_g<4>(a, b, lpp, st);
+        case 2: return glm_ram_wave_g<GlmWaveChain<2>>(a, b, lpp, st);
+        case 4: return glm_ram_wave_g<GlmWaveChain<4>>(a, b, lpp, st);
         default: return hipErrorInvalidValue;
     }
 }

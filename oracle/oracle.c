@@ -667,8 +667,8 @@ static void orc_chain(const orc_model* m, const orc_sampler* s, uint64_t seed, u
             double* Lc = st->ram_L + c;
             orc_normals(seed, chain, (uint32_t)i, d, mom);                    /* rvec = randn(d) */
             double nz = 0.0;                                                  /* dot(rvec, rvec): in order, */
-            if (orc_is_glm(m) && d > 32)                                      /* or in the wave order of the */
-                nz = orc_dot_lanes(mom, d, 1);                                /* wave-per-chain kernels: the */
+            if (orc_is_glm(m) && d > 32)                                      /* or in the lane order of the */
+                nz = orc_dot_lanes(mom, d, d <= 256 ? ORC_ORDER_HALF : 1);    /* wave-per-chain kernels: the */
             else if (order == 0 || order == ORC_ORDER_PAIR || orc_is_glm(m))  /* regression split step (d > 32, */
                 for (int j = 0; j < d; ++j) nz = fma(mom[j], mom[j], nz);     /* glm_ram_wave.hip), separable */
             else                                                              /* targets (d > 32) */

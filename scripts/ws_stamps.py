@@ -44,4 +44,26 @@ out["V"]["tile"] = float(np.median(tile[:, V]))
 out["M"]["bar_p90"] = float(np.percentile(ph[:, M, :, 2], 90))
 out["V"]["bar_p90"] = float(np.percentile(ph[:, V, :, 3], 90))
 out["chains"] = C
+# the workgroup's phases outside the tile loop (per wave: start, proposal barrier, bx / tile-2 barrier, eta_0 barrier,
+# loop end, final barrier, end (M waves only))
+if hasattr(lib, "mcmc_debug_ws_wg"):
+    wg = np.zeros((4, 8, 8), dtype=np.uint32)
+    lib.mcmc_debug_ws_wg.argtypes = [ct.c_void_p]
+    assert lib.mcmc_debug_ws_wg(wg.ctypes.data) == 0
+    w64 = wg.astype(np.int64)
+    dd = np.diff(w64, axis=-1) % (1 << 32)
+    names = ["proposal", "bx_tile2", "eta0", "loop", "final_bar", "finish"]
+    out["wg_M"] = {nm: float(np.median(dd[:, 0:4, i])) for i, nm in enumerate(names)}
+    out["wg_V"] = {nm: float(np.median(dd[:, 4:8, i])) for i, nm in enumerate(names[:5])}
+    out["wg_M"]["total"] = float(np.median((w64[:, 0:4, 6] - w64[:, 0:4, 0]) % (1 << 32)))
+    w2 = np.zeros((4, 8, 4), dtype=np.uint32)
+    lib.mcmc_debug_ws_wg2.argtypes = [ct.c_void_p]
+    assert lib.mcmc_debug_ws_wg2(w2.ctypes.data) == 0
+    w2 = w2.astype(np.int64)
+    st = w64[:, :, 0]
+    out["prop_V"] = {"normals": float(np.median((w2[:, 4:8, 0] - st[:, 4:8]) % (1 << 32))),
+                     "qf_sum": float(np.median((w2[:, 4:8, 1] - w2[:, 4:8, 0]) % (1 << 32))),
+                     "table": float(np.median((w2[:, 4:8, 2] - w2[:, 4:8, 1]) % (1 << 32)))}
+    out["prop_M"] = {"tile0": float(np.median((w2[:, 0:4, 0] - st[:, 0:4]) % (1 << 32))),
+                     "tile1": float(np.median((w2[:, 0:4, 1] - w2[:, 0:4, 0]) % (1 << 32)))}
 print(json.dumps(out))

@@ -639,12 +639,14 @@ def test_glm_ram_parity(gpu, kind, d):
 
 
 @pytest.mark.parametrize("kind,d", [("linear", 33), ("logistic", 64), ("linear", 128), ("probit", 100),
-                                    ("logistic", 300), ("linear", 600), ("linear", 1024)])
+                                    ("logistic", 256), ("linear", 257), ("logistic", 300), ("linear", 600),
+                                    ("linear", 1024)])
 def test_glm_ram_wave_parity(gpu, kind, d):
     """RAM on the regression targets for 32 < d <= 1024 (round 5): per step the regression eval kernel and the
-    wave-per-chain accept / factor-update kernel (glm_ram_wave.hip); samples, accept bits, final state, the
-    evaluation count and every factor bitwise against the oracle (|rvec|^2 in the 64-lane wave order); a tail wave,
-    several launches, a continuation."""
+    wave-per-chain accept / factor-update kernel (glm_ram_wave.hip; two chains a wave for d <= 256, round 6); samples,
+    accept bits, final state, the evaluation count and every factor bitwise against the oracle (|rvec|^2 in the
+    half-wave order for d <= 256, the 64-lane wave order above); 37 chains: a half-live tail wave, several launches,
+    a continuation."""
     m = _glm_model(kind, d, n=40)
     C = 37
     r = mc.SerialMC(steps=12 if d <= 300 else 6, burnin=2, thinning=2)
