@@ -707,6 +707,21 @@ __device__ __forceinline__ void glm_load(const GlmArgs& a, const GlmPos& p, cons
     for (int slot = 0; slot < (4 * NM); ++slot)
         v[slot] = glm_valid(a, p, slot) ? lp[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
 }
+// glm_load with unconditional loads (an invalid slot reads the lane's row 0 and is zeroed): no masked load and wait
+// per slot, every load in flight together -- for kernels that load the state once and have the registers for it
+// (the evaluation kernel); in the step kernels the compiler then keeps the loads live across the step and spills
+template <int NM>
+__device__ __forceinline__ void glm_load_all(const GlmArgs& a, const GlmPos& p, const double* src,
+                                             double (&v)[(4 * NM)]) {
+    const double* lp = glm_lane_ptr(p, src, a.s.ld, p.live ? p.c : 0);
+    const size_t ld = (size_t)a.s.ld;
+#pragma unroll
+    for (int slot = 0; slot < (4 * NM); ++slot) {
+        const bool ok = glm_valid(a, p, slot);
+        const double t = lp[ok ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0];
+        v[slot] = ok ? t : 0.0;
+    }
+}
 template <int NM>
 __device__ __forceinline__ void glm_store(const GlmArgs& a, const GlmPos& p, double* dst, int64_t ldd,
                                           const double (&v)[(4 * NM)]) {
@@ -814,7 +829,7 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_eval_kernel(GlmArgs a, co
     const GlmLds L = glm_lds(a, smem);
     double x[(4 * NM)];
     f64x4 g[NM];
-    glm_load<NM>(a, p, xin, x);
+    glm_load_all<NM>(a, p, xin, x);
     bool oos;
     const double lp = glm_eval<NM, NW, true>(a, p, L, x, g, oos);
     if (p.live && p.q == 0 && p.slice == 0) lp_out[p.c] = lp;
@@ -1187,6 +1202,101 @@ __global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
     glm_count_evals(a, p, s.nsteps);
 }
 
+// ------------------------------------------------------------------ batched proposal normals
+// normals4 (detmath.hpp) of NB Philox blocks, bitwise -- the same operations on the same values -- with every
+// table-row load of the 2 NB radii (bm_radius_u32's main rows) and the 2 NB angles (det_sincos2pi_u32's row) issued
+// before the first is used.  normals4 waits for each radius's rows in turn, and the radius tail branch waits for
+// every load in flight, so a wave drawing a 128-coordinate proposal from the global tables paid about four memory
+// latencies per block; here the rows of all NB blocks are in flight together and only a (rare, 2^-11 per draw) tail
+// lane costs a wait of its own.
+template <int NB>
+__device__ __forceinline__ void normals_batch(const u32x4 (&w)[NB], double (&z)[4 * NB]) {
+    typedef double f64x2_t __attribute__((ext_vector_type(2)));
+    constexpr int NR = 2 * NB;
+    constexpr uint32_t kOff0 = 0u - ((uint32_t)((1023 + 21) << 5) << 4);
+    constexpr uint32_t kOff1 = kOff0 + (uint32_t)(BM_RADP_NROWS / 2) * 16u;
+    uint32_t wr[NR], wa[NR];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        wr[2 * b] = w[b].x; wa[2 * b] = w[b].y;
+        wr[2 * b + 1] = w[b].z; wa[2 * b + 1] = w[b].w;
+    }
+    uint32_t vv[NR], smv[NR];
+    bool tl[NR];
+    double t[NR];
+    f64x2_t c[NR][4];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {                                      // bm_radius_u32: the main-table rows
+        const uint32_t sm = (uint32_t)((int32_t)wr[k] >> 31);
+        const uint32_t v = wr[k] ^ sm;
+        const double y = (double)v;
+        const uint64_t b = d2bits(y);
+        const uint32_t yh = (uint32_t)(b >> 32);
+        tl[k] = v < (1u << 21);
+        const uint32_t sel = (sm & kOff1) | (~sm & kOff0);
+        uint32_t off = ((yh >> 15) << 4) + sel;
+        const uint32_t th = (yh & 0x7fffu) | 0x3ff00000u;
+        off = tl[k] ? 0u : off;
+        t[k] = bits2d(((uint64_t)th << 32) | (b & 0xffffffffull)) - (1.0 + 1.0 / 64.0);
+        const char* base = reinterpret_cast<const char*>(kBmRadPTab) + off;
+        c[k][0] = *reinterpret_cast<const f64x2_t*>(base);
+        c[k][1] = *reinterpret_cast<const f64x2_t*>(base + 16 * BM_RADP_NROWS);
+        c[k][2] = *reinterpret_cast<const f64x2_t*>(base + 32 * BM_RADP_NROWS);
+        c[k][3] = *reinterpret_cast<const f64x2_t*>(base + 48 * BM_RADP_NROWS);
+        vv[k] = v;
+        smv[k] = sm;
+    }
+    int32_t ji[NR];
+    f64x2_t ar[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {                                      // det_sincos2pi_u32: the (sin a, cos a) row
+        ji[k] = ((int32_t)(wa[k] << 10)) >> 10;
+        const uint32_t off = (wa[k] - (uint32_t)ji[k]) >> 18;
+        ar[k] = *reinterpret_cast<const f64x2_t*>(reinterpret_cast<const char*>(kBmSinCos1024Tab) + off);
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {                                      // bm_radius_u32's tail, on the lanes in it
+        if (tl[k]) {
+            uint32_t v2 = vv[k];
+            asm volatile("" : "+v"(v2));
+            const double x = (double)v2 + 0.5;
+            const uint64_t bx = d2bits(x);
+            const uint32_t xh = (uint32_t)(bx >> 32);
+            const uint32_t rw = (uint32_t)((int)(xh >> 15) - ((1023 - 1) << 5)) * 16u +
+                                (smv[k] & (16u * (BM_RADT_NROWS / 2)));
+            t[k] = bits2d(((uint64_t)((xh & 0x7fffu) | 0x3ff00000u) << 32) | (bx & 0xffffffffull)) - (1.0 + 1.0 / 64.0);
+            asm volatile(
+                "global_load_dwordx4 %0, %4, %5\n\t"
+                "global_load_dwordx4 %1, %4, %6\n\t"
+                "global_load_dwordx4 %2, %4, %7\n\t"
+                "global_load_dwordx4 %3, %4, %8\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&v"(c[k][0]), "=&v"(c[k][1]), "=&v"(c[k][2]), "=&v"(c[k][3])
+                : "v"(rw), "s"(&kBmRadTTab[0][0]), "s"(&kBmRadTTab[BM_RADT_NROWS][0]),
+                  "s"(&kBmRadTTab[2 * BM_RADT_NROWS][0]), "s"(&kBmRadTTab[3 * BM_RADT_NROWS][0])
+                : "memory");
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        double q = __builtin_fma(c[k][3].y, t[k], c[k][3].x);           // the radius polynomial
+        q = __builtin_fma(q, t[k], c[k][2].y);
+        q = __builtin_fma(q, t[k], c[k][2].x);
+        q = __builtin_fma(q, t[k], c[k][1].y);
+        q = __builtin_fma(q, t[k], c[k][1].x);
+        q = __builtin_fma(q, t[k], c[k][0].y);
+        const double rad = __builtin_fma(q, t[k], c[k][0].x);
+        const double j = (double)ji[k];                                 // the angle
+        const double j2 = j * j;
+        const double sr = j * __builtin_fma(j2, __builtin_fma(j2, kSinJ5, kSinJ3), kSinJ1);
+        const double cr = __builtin_fma(j2, __builtin_fma(j2, kCosJ4, kCosJ2), 1.0);
+        const double sn = __builtin_fma(ar[k].x, cr, ar[k].y * sr);
+        const double cs = __builtin_fma(ar[k].y, cr, -(ar[k].x * sr));
+        z[2 * k] = rad * cs;
+        z[2 * k + 1] = rad * sn;
+    }
+}
+
 // ------------------------------------------------------------------ wave-specialised single-slice MALA
 // glm_mala1ws<NM>: glm_mala1's step (config 3: logistic MALA, d = 128) with the work of a 16-chain tile split over
 // two waves that share a SIMD (a 512-thread workgroup puts waves w and w + 4 on one SIMD):
@@ -1202,7 +1312,7 @@ __global__ __launch_bounds__(glm_block<1>()) void glm_mala1(GlmArgs a) {
 // there), so the results are glm_mala1's bit for bit and orc_glm_eval restates them.
 // LDS (doubles; XS = glm_tile_doubles(16 NM), X rows then Y): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
 // which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | the logistic term's table
-// (kSoftplusTab) | qf, lik [2][4][16].
+// (kSoftplusTab) | qf, lik [2][4][16] | M's partial qf [4][64].
 template <int NM>
 __host__ __device__ constexpr int glm_ws_region(int XS) {
     return (2 * XS + 4096) > (4 * 4 * NM * 64) ? (2 * XS + 4096) : (4 * 4 * NM * 64);
@@ -1210,7 +1320,7 @@ __host__ __device__ constexpr int glm_ws_region(int XS) {
 __host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
     const int XS = glm_tile_doubles(16 * nm);
     const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
-    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16)
+    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16 + 4 * 64)
 #ifdef GLM_WS_STAMP
            + 512                                               // the phase stamps (dev build, scripts/ws_stamps.py)
 #endif
@@ -1223,7 +1333,7 @@ __host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
 // barrier.  Kept in LDS past the kernel's own and copied out after the loop.
 static __device__ unsigned g_ws_stamps[4][8][16][8];
 static __device__ unsigned g_ws_wg[4][8][8];           // per wave: start, proposal, bx/tile 2, eta_0, loop end, final barrier, end
-static __device__ unsigned g_ws_wg2[4][8][4];          // inside the proposal phase (V: normals done, qf summed, table; M: tiles 0, 1)
+static __device__ unsigned g_ws_wg2[4][8][8];          // inside the proposal phase (V: normals done, qf summed, table; M: tiles 0, 1)
 #define WS_WG2(pt)                                                                                     \
     do {                                                                                               \
         const unsigned ts_ = (unsigned)__builtin_amdgcn_s_memtime();                                  \
@@ -1280,8 +1390,9 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double* const ltabp = Yb + 64;                             // logistic term's table [SP_NROWS][10]
     double* const qfl = ltabp + SP_NROWS * 10;                 // qf [4][16], then lik [4][16]
     double* const likl = qfl + 64;
+    double* const qpart = likl + 64;                           // M's partial qf per lane [4 tiles][64] (proposal phase)
 #ifdef GLM_WS_STAMP
-    unsigned* const wst = reinterpret_cast<unsigned*>(likl + 64);
+    unsigned* const wst = reinterpret_cast<unsigned*>(qpart + 256);
 #endif
     auto xslot = [&](int64_t tt) -> double* { const int b = (int)(tt & 3); return b < 2 ? Xs + b * XS : R + (b - 2) * XS; };
     const Stream rs{s.key0, s.key1};
@@ -1321,46 +1432,60 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     };
     double* const xb = beta + (size_t)(p.tile * NS) * 64 + p.lane;   // this lane's proposal slots
 
-    // ---- proposal phase: V waves draw the proposal (MALA.jl:98-103) into LDS; M waves stage X tiles 0 and 1
+    // ---- proposal phase: the proposal (MALA.jl:98-103) into LDS, its Philox blocks split between the tile's two
+    //      waves (M: m < NM/2, V: the rest; the proposal is latency-bound -- table reads, state loads -- and the M
+    //      waves had only the X tiles 0 and 1 to stage); qf's sum runs in slot order: M's partial over its slots
+    //      crosses to V through LDS and V continues it over its own, so the sum is glm_mala1's
     WS_WG(0);
-    if (vwave) {
-        // every state load unconditional (an invalid slot reads the lane's row 0 and is zeroed): no masked load
-        // and wait per slot, the loads of several slots in flight together
+    constexpr int m_split = NM / 2;
+    double tv[NS];                                             // V: its slots' qf terms, summed after M's partial
+    {
         double qf = 0.0;
+        const double sq = __builtin_sqrt(h);
+        // the wave's blocks [M0, M1): the blocks' normals with their table rows in flight together, then the state
+        // (every load unconditional: an invalid slot reads the lane's row 0 and is zeroed)
+        auto part = [&](auto m0c, auto m1c) {
+            constexpr int M0 = decltype(m0c)::value, M1 = decltype(m1c)::value, NBK = M1 - M0;
+            if constexpr (NBK > 0) {
+                u32x4 w[NBK];
 #pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            const uint32_t blk = (uint32_t)(4 * m + p.q);                    // coords 4*blk .. 4*blk+3
-            const u32x4 w = rs.block(chain, (uint32_t)i, blk, TAG_NORMAL);
-            double z[4];
-            normals4(w, z[0], z[1], z[2], z[3]);
-            const double sq = __builtin_sqrt(h);
+                for (int b = 0; b < NBK; ++b)                                  // coords 4*blk .. 4*blk+3
+                    w[b] = rs.block(chain, (uint32_t)i, (uint32_t)(4 * (M0 + b) + p.q), TAG_NORMAL);
+                double z[4 * NBK];
+                normals_batch<NBK>(w, z);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int slot = 4 * m + e;
-                const bool v = glm_valid(a, p, slot);
-                const size_t o = v ? (size_t)(16 * m + e) * ld : 0;
-                const double xl0 = xl[o], gl0 = gl[o];
-                const double xv = v ? xl0 : 0.0;
-                const double gv = v ? gl0 : 0.0;
-                const double pm = xv + half * gv;                               // MALA.jl:98
-                const double xpv = pm + sq * (v ? z[e] : 0.0);                  // MALA.jl:100
-                const double ee = pm - xpv;
-                if (v) qf = qf + ((-(ee * ee)) / twoh - Lc);                    // MALA.jl:103
-                xb[64 * slot] = xpv;
+                for (int k = 0; k < 4 * NBK; ++k) {
+                    const int slot = 4 * M0 + k;
+                    const bool v = glm_valid(a, p, slot);
+                    const size_t o = v ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0;
+                    // global loads (as flat loads, each LDS store of the proposal below would wait for them all)
+                    typedef const __attribute__((address_space(1))) double gdouble;
+                    const double xl0 = *(gdouble*)(xl + o), gl0 = *(gdouble*)(gl + o);
+                    const double xv = v ? xl0 : 0.0;
+                    const double gv = v ? gl0 : 0.0;
+                    const double pm = xv + half * gv;                           // MALA.jl:98
+                    const double xpv = pm + sq * (v ? z[k] : 0.0);              // MALA.jl:100
+                    const double ee = pm - xpv;
+                    const double term = (-(ee * ee)) / twoh - Lc;               // MALA.jl:103
+                    if (vwave) tv[slot] = term;
+                    else if (v) qf = qf + term;
+                    xb[64 * slot] = xpv;
+                }
             }
-        }
+        };
+        if (vwave) part(std::integral_constant<int, NM / 2>{}, std::integral_constant<int, NM>{});
+        else part(std::integral_constant<int, 0>{}, std::integral_constant<int, NM / 2>{});
         WS_WG2(0);
-        qf = glm_sum(a, p, GlmLds{}, qf);
-        if (p.q == 0) qfl[p.tile * 16 + p.cl] = qf;
-        WS_WG2(1);
+        if (!vwave) qpart[p.tile * 64 + p.lane] = qf;
+    }
+    if (vwave) {
         if (logi) {
             for (int e = u; e < SP_NROWS * 10; e += 256) ltabp[e] = (&kSoftplusTab[0][0])[e];
         }
-        WS_WG2(2);
+        WS_WG2(1);
     } else {
         load_tile(0);
         store_tile(0);
-        WS_WG2(0);
         if (ntiles > 1) {
             load_tile(1);
             store_tile(1);
@@ -1369,7 +1494,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     }
     __syncthreads();
     WS_WG(1);
-    // ---- M: the proposal into registers, eta_0;  V: X tile 2 into registers (slot 2 overlays the proposal)
+    // ---- M: the proposal into registers, eta_0;  V: qf, X tile 2 into registers (slot 2 overlays the proposal)
     double bx[NS];
     f64x4 G[NM];
     if (!vwave) {
@@ -1377,8 +1502,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         for (int slot = 0; slot < NS; ++slot) bx[slot] = xb[64 * slot];
 #pragma unroll
         for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
-    } else if (ntiles > 2) {
-        load_tile(2);
+    } else {
+        double qf = qpart[p.tile * 64 + p.lane];
+#pragma unroll
+        for (int slot = 4 * m_split; slot < NS; ++slot)
+            if (glm_valid(a, p, slot)) qf = qf + tv[slot];
+        qf = glm_sum(a, p, GlmLds{}, qf);
+        if (p.q == 0) qfl[p.tile * 16 + p.cl] = qf;
+        WS_WG2(2);
+        if (ntiles > 2) load_tile(2);
     }
     __syncthreads();                                           // the proposal area is free from here on
     WS_WG(2);
@@ -1519,10 +1651,11 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     if (vwave) return;
     // ---- M waves: the end of the evaluation (glm_finish), MALA.jl:104-125
     // the current position (qb, and the kept rows of a rejected step), every load unconditional and issued first
+    typedef const __attribute__((address_space(1))) double gdouble;   // global, not flat, loads (see the proposal)
     double xo[NS];
 #pragma unroll
     for (int slot = 0; slot < NS; ++slot)
-        xo[slot] = xl[glm_valid(a, p, slot) ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0];
+        xo[slot] = *(gdouble*)(xl + (glm_valid(a, p, slot) ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0));
     double lp = a.st.lp[cc];
     int32_t n_acc = sa.tuner ? a.st.t_acc[cc] : 0;
     int32_t n_prop = sa.tuner ? a.st.t_prop[cc] : 0;
@@ -1555,6 +1688,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
             G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - bx[slot]) / s2p + G[slot >> 2][slot & 3];
         lpp = acc;                                                          // MALA.jl:101
     }
+    WS_WG2(3);
     (void)oos;
     double qb = 0.0;
 #pragma unroll
@@ -1565,8 +1699,10 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         if (v) qb = qb + ((-(e * e)) / twoh - Lc);
     }
     qb = glm_sum(a, p, GlmLds{}, qb);
+    WS_WG2(4);
     const double ratio = ((lpp + qb) - lp) - qf;                   // MALA.jl:107
     const bool acc = glm_mh_short_circuit(rs, chain, (uint32_t)i, ratio);
+    WS_WG2(5);
     int64_t kk;
     const bool kept = kept_index(i - s.run_step0, s.burnin, s.thinning, s.len, &kk);
     double* const ks = kept && s.samples ? s.samples + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
@@ -1587,13 +1723,14 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                 gw[r * ld] = gv;
             } else {
                 xv = xo[slot];
-                gv = gl[r * ld];
+                gv = *(gdouble*)(gl + r * ld);
             }
             const size_t ko = (size_t)(4 * p.q + r) * Cs + (size_t)p.c;
             if (ks) ks[ko] = xv;
             if (kg) kg[ko] = gv;
         }
     }
+    WS_WG2(6);
     double hn = h;
     if (acc) {
         lp = lpp;

@@ -56,14 +56,20 @@ if hasattr(lib, "mcmc_debug_ws_wg"):
     out["wg_M"] = {nm: float(np.median(dd[:, 0:4, i])) for i, nm in enumerate(names)}
     out["wg_V"] = {nm: float(np.median(dd[:, 4:8, i])) for i, nm in enumerate(names[:5])}
     out["wg_M"]["total"] = float(np.median((w64[:, 0:4, 6] - w64[:, 0:4, 0]) % (1 << 32)))
-    w2 = np.zeros((4, 8, 4), dtype=np.uint32)
+    w2 = np.zeros((4, 8, 8), dtype=np.uint32)
     lib.mcmc_debug_ws_wg2.argtypes = [ct.c_void_p]
     assert lib.mcmc_debug_ws_wg2(w2.ctypes.data) == 0
     w2 = w2.astype(np.int64)
     st = w64[:, :, 0]
-    out["prop_V"] = {"normals": float(np.median((w2[:, 4:8, 0] - st[:, 4:8]) % (1 << 32))),
+    out["prop_V"] = {"normals": float(np.median((w2[:, 4:8, 0] - st[:, 4:8]) % (1 << 32))), "M_normals": float(np.median((w2[:, 0:4, 0] - st[:, 0:4]) % (1 << 32))),
                      "qf_sum": float(np.median((w2[:, 4:8, 1] - w2[:, 4:8, 0]) % (1 << 32))),
                      "table": float(np.median((w2[:, 4:8, 2] - w2[:, 4:8, 1]) % (1 << 32)))}
+    fin0 = w64[:, 0:4, 5]                                     # M: the final barrier passed
+    out["finish_M"] = {"llacc": float(np.median((w2[:, 0:4, 3] - fin0) % (1 << 32))),
+                       "qb": float(np.median((w2[:, 0:4, 4] - w2[:, 0:4, 3]) % (1 << 32))),
+                       "accept": float(np.median((w2[:, 0:4, 5] - w2[:, 0:4, 4]) % (1 << 32))),
+                       "stores": float(np.median((w2[:, 0:4, 6] - w2[:, 0:4, 5]) % (1 << 32))),
+                       "rest": float(np.median((w64[:, 0:4, 6] - w2[:, 0:4, 6]) % (1 << 32)))}
     out["prop_M"] = {"tile0": float(np.median((w2[:, 0:4, 0] - st[:, 0:4]) % (1 << 32))),
                      "tile1": float(np.median((w2[:, 0:4, 1] - w2[:, 0:4, 0]) % (1 << 32)))}
 print(json.dumps(out))
