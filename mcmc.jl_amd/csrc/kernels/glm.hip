@@ -1356,7 +1356,7 @@ static __device__ unsigned g_ws_wg2[4][8][8];          // inside the proposal ph
 #define WS_WG(pt) do { } while (0)
 #define WS_WG2(pt) do { } while (0)
 #endif
-template <int NM>
+template <int NM, bool UNITP = false>
 __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int NS = 4 * NM;
@@ -1667,13 +1667,28 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         const int d = M.d;
         const double lik = likl[p.tile * 16 + p.cl];
         const double sp = M.prior_sigma, s2p = sp * sp, logsp = det_log(sp);
+        // the prior's divisions by sigma and sigma^2 (vars ~ Normal(0, sigma)) are exact no-ops at sigma = 1 (the
+        // examples' prior, x / 1 == x for every double): the UNITP instance (launched when prior_sigma == 1) skips
+        // them, bitwise the same (64 IEEE divisions a lane, a third of this phase)
+        constexpr bool unit = UNITP;
         double pp = 0.0;
+        if (unit) {
 #pragma unroll
-        for (int slot = 0; slot < NS; ++slot) {
-            const int k = own_coord(p, slot);
-            if (k < d) {
-                const double z = (bx[slot] - 0.0) / sp;
-                pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
+            for (int slot = 0; slot < NS; ++slot) {
+                const int k = own_coord(p, slot);
+                if (k < d) {
+                    const double z = bx[slot] - 0.0;
+                    pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int slot = 0; slot < NS; ++slot) {
+                const int k = own_coord(p, slot);
+                if (k < d) {
+                    const double z = (bx[slot] - 0.0) / sp;
+                    pp = pp + (-0.5 * (z * z + kLog2Pi) - logsp);
+                }
             }
         }
         const double prior = glm_sum(a, p, GlmLds{}, pp);
@@ -1683,9 +1698,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         bad = bad || !(acc - acc == 0.0);
         oos = bad;
         if (bad) acc = -__builtin_inf();
+        if (unit) {
 #pragma unroll
-        for (int slot = 0; slot < NS; ++slot)
-            G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - bx[slot]) / s2p + G[slot >> 2][slot & 3];
+            for (int slot = 0; slot < NS; ++slot)
+                G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - bx[slot]) + G[slot >> 2][slot & 3];
+        } else {
+#pragma unroll
+            for (int slot = 0; slot < NS; ++slot)
+                G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - bx[slot]) / s2p + G[slot >> 2][slot & 3];
+        }
         lpp = acc;                                                          // MALA.jl:101
     }
     WS_WG2(3);
@@ -1708,26 +1729,30 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double* const ks = kept && s.samples ? s.samples + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
     double* const kg = kept && s.grads ? s.grads + (size_t)kk * (size_t)s.d * (size_t)s.C : nullptr;
     if (p.live) {
+        // an accepted proposal is the new state; a rejected one leaves the state in HBM as it is.  Kept steps (one in
+        // `thinning`, wave-uniform) write the rows, a rejected lane's gradient reloaded in groups of 8 slots with
+        // every load unconditional (a masked load per slot waited for each in turn)
         double* const xw = a.st.x + (size_t)(4 * p.q) * ld + (size_t)p.c;
         double* const gw = a.st.g + (size_t)(4 * p.q) * ld + (size_t)p.c;
         const size_t Cs = (size_t)s.C;
+        if (acc) {
 #pragma unroll
-        for (int slot = 0; slot < NS; ++slot) {
-            if (!glm_valid(a, p, slot)) continue;
-            const size_t r = (size_t)(16 * (slot >> 2) + (slot & 3));
-            double xv, gv;
-            if (acc) {
-                xv = bx[slot];
-                gv = G[slot >> 2][slot & 3];
-                xw[r * ld] = xv;
-                gw[r * ld] = gv;
-            } else {
-                xv = xo[slot];
-                gv = *(gdouble*)(gl + r * ld);
+            for (int slot = 0; slot < NS; ++slot) {
+                if (!glm_valid(a, p, slot)) continue;
+                const size_t r = (size_t)(16 * (slot >> 2) + (slot & 3));
+                xw[r * ld] = bx[slot];
+                gw[r * ld] = G[slot >> 2][slot & 3];
             }
-            const size_t ko = (size_t)(4 * p.q + r) * Cs + (size_t)p.c;
-            if (ks) ks[ko] = xv;
-            if (kg) kg[ko] = gv;
+        }
+        if (ks || kg) {
+#pragma unroll
+            for (int slot = 0; slot < NS; ++slot) {
+                if (!glm_valid(a, p, slot)) continue;
+                const size_t r = (size_t)(16 * (slot >> 2) + (slot & 3));
+                const size_t ko = (size_t)(4 * p.q + r) * Cs + (size_t)p.c;
+                if (ks) ks[ko] = acc ? bx[slot] : xo[slot];
+                if (kg) kg[ko] = acc ? G[slot >> 2][slot & 3] : *(gdouble*)(gl + r * ld);
+            }
         }
     }
     WS_WG2(6);
@@ -1958,11 +1983,15 @@ hipError_t mcmc_launch_glm_mala1(int nm, const mcmc::GlmArgs& a, size_t lds, dim
 #if GLM_MALA1_WS
     (void)lds;
     const size_t lw = glm_ws_lds_doubles(a.g.nm) * sizeof(double);
+    const bool unit = a.m.prior_sigma == 1.0;                 // the prior's divisions are exact no-ops (glm_mala1ws)
     switch (nm) {
         case 1: glm_mala1ws<1><<<grid, 512, lw, st>>>(a); break;
         case 2: glm_mala1ws<2><<<grid, 512, lw, st>>>(a); break;
         case 4: glm_mala1ws<4><<<grid, 512, lw, st>>>(a); break;
-        case 8: glm_mala1ws<8><<<grid, 512, lw, st>>>(a); break;
+        case 8:
+            if (unit) glm_mala1ws<8, true><<<grid, 512, lw, st>>>(a);
+            else glm_mala1ws<8><<<grid, 512, lw, st>>>(a);
+            break;
         default: return hipErrorInvalidValue;
     }
 #else

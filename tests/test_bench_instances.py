@@ -186,14 +186,17 @@ def test_few_chain_rwm_models_and_sizes(gpu, C, d):
 
 @pytest.mark.parametrize("tuned", [False, True])
 @pytest.mark.parametrize("link_sign", [1.0, -1.0])
-def test_config3_logistic_mala_instance(gpu, tuned, link_sign):
+@pytest.mark.parametrize("prior", [1.0, 2.5])
+def test_config3_logistic_mala_instance(gpu, tuned, link_sign, prior):
     """config 3's kernel: logistic regression n=1000, d=128 under MALA(0.001) (test/test_syntax.jl:28's sampler),
     the wave-specialised glm_mala1ws<8> (M and V waves on one SIMD); 200 chains (a partial 64-chain workgroup),
-    bitwise against the oracle over several launches (one step per launch), tuned and untuned, both link signs."""
+    bitwise against the oracle over several launches (one step per launch), tuned and untuned, both link signs, the
+    unit prior (its instance skips the exact x / 1 divisions) and another."""
     from test_gpu_parity import _glm_model
     m0 = _glm_model("logistic", 128, n=1000)
     X, Y = m0.target.X, m0.target.Y
-    m = mc.model(mc.LogisticRegression(X, Y, link_sign=link_sign), vars=np.zeros(128), gradient=True)
+    m = mc.model(mc.LogisticRegression(X, Y, prior_sigma=prior, link_sign=link_sign), vars=np.zeros(128),
+                 gradient=True)
     smp = (lambda: mc.MALA(0.001, mc.EmpMCTuner(0.6, adaptStep=2))) if tuned else (lambda: mc.MALA(0.001))
     r = mc.SerialMC(steps=5, burnin=1, thinning=2)
     t = (m * smp() * r).batch(200, seed=31)
