@@ -41,9 +41,10 @@ hipError_t mcmc_launch_glm_eval(const mcmc::KernelArgs& a, const double* xin, do
                                 hipStream_t st);
 int mcmc_glm_max_d();
 // RAM on regression targets, 32 < d <= 1024 (glm_ram_wave.hip): per step the eval kernel and the accept / factor-update
-// kernel; u [C][ustride], nz [C], xprop [d][ld], lpp [C] are the device buffers between them
+// kernel; u [C][ustride], nz [C], xprop [d][ld], lpp [C] are the device buffers between them.  st2 (may be null):
+// a second stream on which half of a large batch runs, forked from and joined back to st by the two events
 hipError_t mcmc_launch_glm_ram_wave(const mcmc::KernelArgs& a, double* u, double* nz, double* xprop, double* lpp,
-                                    hipStream_t st);
+                                    hipStream_t st, hipStream_t st2, hipEvent_t ev_fork, hipEvent_t ev_join);
 int64_t mcmc_glm_ram_wave_ustride(int d);
 // SeqMC population bookkeeping (seqmc.hip)
 hipError_t mcmc_seqmc_weights(int64_t N, double* logW, const double* ll0, double* logtarget, const double* plogtarget,

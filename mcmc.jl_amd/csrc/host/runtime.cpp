@@ -69,6 +69,10 @@ struct mcmc_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int32_t* d_err = nullptr;
+    // a second stream for launch sequences that split a batch in two halves whose kernels bind on different resources
+    // (RAM on regression targets: the MFMA eval of one half beside the HBM-bound factor update of the other)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 struct mcmc_model {
@@ -194,6 +198,9 @@ extern "C" int mcmc_ctx_create(int device, mcmc_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_err, sizeof(int32_t));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
         delete c;
         return fail(MCMC_E_HIP, std::string("context creation: ") + hipGetErrorString(e));
@@ -209,6 +216,10 @@ extern "C" int mcmc_ctx_destroy(mcmc_ctx* ctx) {
     dfree(ctx->d_err);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MCMC_OK;
@@ -617,7 +628,11 @@ static void free_state(mcmc_chains* c) {
 
 // the step kernels of one launch; RAM on a regression target with d > 32 is a sequence of kernels per step
 static hipError_t launch_chain_step(const mcmc_chains* c, const KernelArgs& a, hipStream_t st) {
-    if (c->glm_ram_wave) return mcmc_launch_glm_ram_wave(a, c->ram_u, c->ram_nz, c->xprop, c->lpp, st);
+    if (c->glm_ram_wave) {
+        const mcmc_ctx* ctx = c->model->ctx;
+        return mcmc_launch_glm_ram_wave(a, c->ram_u, c->ram_nz, c->xprop, c->lpp, st,
+                                        st == ctx->stream ? ctx->stream2 : nullptr, ctx->ev_fork, ctx->ev_join);
+    }
     return launch_step(c->layout, a, st);
 }
 

@@ -698,6 +698,13 @@ __device__ __forceinline__ T* glm_lane_ptr(const GlmPos& p, T* base, int64_t ld,
 __device__ __forceinline__ bool glm_valid(const GlmArgs& a, const GlmPos& p, int slot) {
     return own_coord(p, slot) < a.s.d;
 }
+// an unconditional load's offset from the lane pointer (row base + 4q of the chain) to slot `slot`'s row, or, for a
+// slot past d, to the chain's row 0: the state holds d rows, and the lane's own row base + 4q is past them too when
+// d is not a multiple of the slice geometry (d = 300: rows 300..511; the loaded value is zeroed either way)
+__device__ __forceinline__ ptrdiff_t glm_slot_off(const GlmArgs& a, const GlmPos& p, int slot, size_t ld) {
+    return glm_valid(a, p, slot) ? (ptrdiff_t)(16 * (slot >> 2) + (slot & 3)) * (ptrdiff_t)ld
+                                 : -(ptrdiff_t)(p.base + 4 * p.q) * (ptrdiff_t)ld;
+}
 template <int NM>
 __device__ __forceinline__ void glm_load(const GlmArgs& a, const GlmPos& p, const double* src,
                                          double (&v)[(4 * NM)]) {
@@ -707,7 +714,7 @@ __device__ __forceinline__ void glm_load(const GlmArgs& a, const GlmPos& p, cons
     for (int slot = 0; slot < (4 * NM); ++slot)
         v[slot] = glm_valid(a, p, slot) ? lp[(size_t)(16 * (slot >> 2) + (slot & 3)) * ld] : 0.0;
 }
-// glm_load with unconditional loads (an invalid slot reads the lane's row 0 and is zeroed): no masked load and wait
+// glm_load with unconditional loads (an invalid slot reads the chain's row 0 and is zeroed): no masked load and wait
 // per slot, every load in flight together -- for kernels that load the state once and have the registers for it
 // (the evaluation kernel); in the step kernels the compiler then keeps the loads live across the step and spills
 template <int NM>
@@ -718,7 +725,7 @@ __device__ __forceinline__ void glm_load_all(const GlmArgs& a, const GlmPos& p, 
 #pragma unroll
     for (int slot = 0; slot < (4 * NM); ++slot) {
         const bool ok = glm_valid(a, p, slot);
-        const double t = lp[ok ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0];
+        const double t = lp[glm_slot_off(a, p, slot, ld)];
         v[slot] = ok ? t : 0.0;
     }
 }
@@ -1312,7 +1319,7 @@ __device__ __forceinline__ void normals_batch(const u32x4 (&w)[NB], double (&z)[
 // there), so the results are glm_mala1's bit for bit and orc_glm_eval restates them.
 // LDS (doubles; XS = glm_tile_doubles(16 NM), X rows then Y): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
 // which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | the logistic term's table
-// (kSoftplusTab) | qf, lik [2][4][16] | M's partial qf [4][64].
+// (kSoftplusTab) | qf, lik [2][4][16] | M's partial qf [4][64] | row 3's term [2][4][64] and bound [4][64] (logistic).
 template <int NM>
 __host__ __device__ constexpr int glm_ws_region(int XS) {
     return (2 * XS + 4096) > (4 * 4 * NM * 64) ? (2 * XS + 4096) : (4 * 4 * NM * 64);
@@ -1320,7 +1327,7 @@ __host__ __device__ constexpr int glm_ws_region(int XS) {
 __host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
     const int XS = glm_tile_doubles(16 * nm);
     const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
-    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16 + 4 * 64)
+    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16 + 4 * 64 + 512 + 256)
 #ifdef GLM_WS_STAMP
            + 512                                               // the phase stamps (dev build, scripts/ws_stamps.py)
 #endif
@@ -1391,8 +1398,10 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double* const qfl = ltabp + SP_NROWS * 10;                 // qf [4][16], then lik [4][16]
     double* const likl = qfl + 64;
     double* const qpart = likl + 64;                           // M's partial qf per lane [4 tiles][64] (proposal phase)
+    double* const T3 = qpart + 256;                            // logistic: row 3's term [2][4 tiles][64] (M -> V)
+    double* const U3 = T3 + 512;                               // ... and the M wave's bound max [4 tiles][64]
 #ifdef GLM_WS_STAMP
-    unsigned* const wst = reinterpret_cast<unsigned*>(qpart + 256);
+    unsigned* const wst = reinterpret_cast<unsigned*>(U3 + 256);
 #endif
     auto xslot = [&](int64_t tt) -> double* { const int b = (int)(tt & 3); return b < 2 ? Xs + b * XS : R + (b - 2) * XS; };
     const Stream rs{s.key0, s.key1};
@@ -1443,7 +1452,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         double qf = 0.0;
         const double sq = __builtin_sqrt(h);
         // the wave's blocks [M0, M1): the blocks' normals with their table rows in flight together, then the state
-        // (every load unconditional: an invalid slot reads the lane's row 0 and is zeroed)
+        // (every load unconditional: an invalid slot reads the chain's row 0 and is zeroed)
         auto part = [&](auto m0c, auto m1c) {
             constexpr int M0 = decltype(m0c)::value, M1 = decltype(m1c)::value, NBK = M1 - M0;
             if constexpr (NBK > 0) {
@@ -1457,7 +1466,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                 for (int k = 0; k < 4 * NBK; ++k) {
                     const int slot = 4 * M0 + k;
                     const bool v = glm_valid(a, p, slot);
-                    const size_t o = v ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0;
+                    const ptrdiff_t o = glm_slot_off(a, p, slot, ld);
                     // global loads (as flat loads, each LDS store of the proposal below would wait for them all)
                     typedef const __attribute__((address_space(1))) double gdouble;
                     const double xl0 = *(gdouble*)(xl + o), gl0 = *(gdouble*)(gl + o);
@@ -1530,8 +1539,9 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         }
         return e;
     };
-    auto g_of = [&](int64_t tt) {                              // G += X_tt^T r_tt (glm_eval1_tiles' G product)
-        const f64x4 rv = Rq[256 * (tt & 1)];
+    auto g_of = [&](int64_t tt, double r3) {                   // G += X_tt^T r_tt (glm_eval1_tiles' G product)
+        f64x4 rv = Rq[256 * (tt & 1)];
+        if (logi) rv[3] = r3;                                  // row 3's weight: the M wave's own (logistic)
         const double* gcol = xslot(tt) + p.q * S + 4 * (p.cl & 3) + (p.cl >> 2);
         double ga[NM];
 #pragma unroll
@@ -1563,17 +1573,46 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     // one loop per role, each with one barrier per tile (the same count): the roles' loop invariants (the V waves'
     // polynomial constants, the M waves' operand addresses) stay out of each other's register pressure
     double lik_part = 0.0;
+    double g3 = 0.0;                                           // M: the last tile's row-3 weight
     double ubnd = -__builtin_inf();                            // logistic: max of u + b over the lane's observations
+    // logistic: the M wave takes row 3 of each tile's elementwise work (the V wave rows 0..2).  The M wave has waited
+    // ~1 600 cycles a tile at the barrier for the V wave's terms, which ran mostly after the MFMAs stopped (the two do
+    // not co-issue on a SIMD); with two waves on the elementwise work its latency overlaps.  Row 3's term crosses to
+    // the V wave through LDS (T3, by tile parity) and is added first in the next tile, so the lane's terms still sum
+    // in (t, r) order; its weight stays in the M wave for G; the bound's max is combined after the loop.
     if (!vwave) {
+        f64x4 eta_t = Eq[0];                                   // eta_0, from the registers it was stored from
+        double rv3 = 0.0;                                      // row 3's weight of tile t - 1 (G_{t-1})
+        double ub3 = -__builtin_inf();
         for (int64_t t = 0; t < ntiles; ++t) {
             WS_STAMP(0);
-            if (t + 1 < ntiles) Eq[256 * ((t + 1) & 1)] = eta_of(t + 1);
+            f64x4 eta_n = eta_t;
+            if (t + 1 < ntiles) {
+                eta_n = eta_of(t + 1);
+                Eq[256 * ((t + 1) & 1)] = eta_n;
+            }
             WS_STAMP(1);
-            if (t >= 1) g_of(t - 1);
+            if (t >= 1) g_of(t - 1, rv3);
             WS_STAMP(2);
+            if (logi) {
+                const double* X0 = xslot(t);
+                const double w3 = X0[YO + p.q + 12];
+                LogiState E;
+                det_logi_s1(eta_t[3], w3, E, sptab);
+                ub3 = __builtin_fmax(ub3, E.u + X0[BO + p.q + 12]);               // the reference's -Inf
+                det_logi_s2(E);
+                double term3, r3;
+                det_logi_fin(E, w3, term3, r3);
+                const bool in = t < nfull || t * 16 + p.q + 12 < M.n;
+                rv3 = in ? r3 : 0.0;
+                T3[256 * (t & 1) + p.tile * 64 + p.lane] = term3;
+                if (t + 1 == ntiles) U3[p.tile * 64 + p.lane] = ub3;
+            }
+            eta_t = eta_n;
             __syncthreads();
             WS_STAMP(3);
         }
+        g3 = rv3;
     } else {
         for (int64_t t = 0; t < ntiles; ++t) {
             WS_STAMP(0);
@@ -1588,23 +1627,34 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
             if (logi) {
-                // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111)
+                // row 3 of tile t - 1 (the M wave's), before this tile's rows: the (t, r) order
+                if (t >= 1 && (t - 1 < nfull || (t - 1) * 16 + p.q + 12 < M.n))
+                    lik_part = lik_part + T3[256 * ((t - 1) & 1) + p.tile * 64 + p.lane];
+                // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111);
+                // rows 0..2 here, row 3 in the M wave
                 const double* LB = xslot(t) + BO;
-                // two rows at a time: four rows' coefficient rows in flight at once spill the wave's registers
-#pragma unroll
-                for (int h = 0; h < 4; h += 2) {
+                {
                     LogiState E[2];
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
-                        det_logi_s1(eta[h + r], y[h + r], E[r], sptab);
-                        ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * (h + r)]);   // the reference's -Inf
+                        det_logi_s1(eta[r], y[r], E[r], sptab);
+                        ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * r]);      // the reference's -Inf
                     }
 #pragma unroll
                     for (int r = 0; r < 2; ++r) det_logi_s2(E[r]);
 #pragma unroll
-                    for (int r = 0; r < 2; ++r) det_logi_fin(E[r], y[h + r], term[h + r], rv[h + r]);
+                    for (int r = 0; r < 2; ++r) det_logi_fin(E[r], y[r], term[r], rv[r]);
                     __builtin_amdgcn_sched_barrier(0);
                 }
+                {
+                    LogiState E;
+                    det_logi_s1(eta[2], y[2], E, sptab);
+                    ubnd = __builtin_fmax(ubnd, E.u + LB[p.q + 8]);
+                    det_logi_s2(E);
+                    det_logi_fin(E, y[2], term[2], rv[2]);
+                }
+                term[3] = 0.0;
+                rv[3] = 0.0;
             } else if (M.kind == MK_PROBIT) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) glm_probit_obs(eta[r], y[r], term[r], rv[r]);
@@ -1617,12 +1667,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                     rv[r] = resid * is2n;
                 }
             }
+            const int nr = logi ? 3 : 4;                                           // logistic: row 3 in the M wave
             if (t < nfull) {                                                       // uniform: no padded observation
 #pragma unroll
-                for (int r = 0; r < 4; ++r) lik_part = lik_part + term[r];         // the lane's terms in (t, r) order
+                for (int r = 0; r < 4; ++r)
+                    if (r < nr) lik_part = lik_part + term[r];                     // the lane's terms in (t, r) order
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+                    if (r >= nr) continue;
                     const bool in = t * 16 + p.q + 4 * r < M.n;
                     lik_part = in ? lik_part + term[r] : lik_part;
                     rv[r] = in ? rv[r] : 0.0;
@@ -1641,10 +1694,15 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         for (int j = p.lane; j < 128; j += 64) (&g_ws_stamps[blockIdx.x][wv][0][0])[j] = wst[wv * 128 + j];
 #endif
     if (vwave) {
+        if (logi) {                                            // the last tile's row 3 and the M wave's bound
+            const int64_t tl = ntiles - 1;
+            if (tl < nfull || tl * 16 + p.q + 12 < M.n) lik_part = lik_part + T3[256 * (tl & 1) + p.tile * 64 + p.lane];
+            ubnd = __builtin_fmax(ubnd, U3[p.tile * 64 + p.lane]);
+        }
         const double lik = glm_sum(a, p, GlmLds{}, logi && ubnd >= 0.0 ? -__builtin_inf() : lik_part);
         if (p.q == 0) likl[p.tile * 16 + p.cl] = lik;
     } else {
-        g_of(ntiles - 1);
+        g_of(ntiles - 1, g3);
     }
     __syncthreads();
     WS_WG(5);
@@ -1655,7 +1713,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double xo[NS];
 #pragma unroll
     for (int slot = 0; slot < NS; ++slot)
-        xo[slot] = *(gdouble*)(xl + (glm_valid(a, p, slot) ? (size_t)(16 * (slot >> 2) + (slot & 3)) * ld : 0));
+        xo[slot] = *(gdouble*)(xl + glm_slot_off(a, p, slot, ld));
     double lp = a.st.lp[cc];
     int32_t n_acc = sa.tuner ? a.st.t_acc[cc] : 0;
     int32_t n_prop = sa.tuner ? a.st.t_prop[cc] : 0;

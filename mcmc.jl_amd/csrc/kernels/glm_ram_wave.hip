@@ -30,7 +30,13 @@ struct GlmChain : B {
     static constexpr int NC = Base::NC;
     static constexpr int CPW = 64 / Base::L;                    // chains per wave
     int64_t ld;
-    __device__ explicit GlmChain(const StepArgs& s) : Base(s) { ld = s.ld; }
+    // c0: the first chain of the launch (a half of the batch on its own stream): the policy's chain index is local
+    // to the launch's grid, every array is indexed by the batch's
+    __device__ GlmChain(const StepArgs& s, int64_t c0) : Base(s) {
+        ld = s.ld;
+        c += c0;
+        live = c < s.C;
+    }
     __device__ __forceinline__ int64_t cc() const { return live ? c : 0; }
     // the wave's first chain (its factor block starts the buffer resource) and this lane's byte offset in it
     __device__ __forceinline__ int64_t wave_chain0() const { return c - (int64_t)((threadIdx.x & 63) / Base::L); }
@@ -68,6 +74,7 @@ struct GlmRamBufs {
     double* xprop;      // [d][ld]
     const double* lpp;  // [C]
     int64_t ustride;    // doubles of u per chain (mcmc_glm_ram_wave_ustride)
+    int64_t c0;         // the launch's first chain (0, or the second half's on the second stream)
 };
 
 // the wave's chains exist (a tail wave with none leaves; with two chains a wave one half may be past C: its loads
@@ -82,7 +89,7 @@ template <class P>
 __global__ __launch_bounds__(kBlock) void glm_ram_prop(KernelArgs a, GlmRamBufs b) {
     constexpr int NC = P::NC, L = P::L, CPW = P::CPW;
     const StepArgs& s = a.s;
-    const P p(s);
+    const P p(s, b.c0);
     if (!glm_ram_wave_live(p, s)) return;                        // wave-uniform
     __shared__ double xpose[kBlock / 64][64 * NC];
     double* const slice = &xpose[threadIdx.x >> 6][((threadIdx.x & 63) / L) * L * NC];
@@ -122,7 +129,7 @@ __global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBuf
     constexpr int NC = P::NC, L = P::L, CPW = P::CPW;
     const StepArgs& s = a.s;
     const SamplerArgs& sa = a.sa;
-    const P p(s);
+    const P p(s, b.c0);
     if (!glm_ram_wave_live(p, s)) return;                        // wave-uniform
     __shared__ double xpose[kBlock / 64][64 * NC];
     double* const slice = &xpose[threadIdx.x >> 6][((threadIdx.x & 63) / L) * L * NC];
@@ -186,23 +193,57 @@ __global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBuf
     }
 }
 
+// batches of at least this many chains run as two halves on two streams (the eval kernel of one half beside the
+// factor update of the other: MFMA and HBM); each half still fills the GPU
+constexpr int64_t kRamTwoStreamMin = 8192;
+
 template <class P>
-static hipError_t glm_ram_wave_g(const KernelArgs& a0, const GlmRamBufs& b0, double* lpp, hipStream_t st) {
+static hipError_t glm_ram_wave_g(const KernelArgs& a0, const GlmRamBufs& b0, double* lpp, hipStream_t st,
+                                 hipStream_t st2, hipEvent_t ev_fork, hipEvent_t ev_join) {
     const int64_t cpb = (int64_t)kChainsPerBlock * P::CPW;     // chains per 256-thread block
-    const dim3 grid((unsigned)((a0.s.C + cpb - 1) / cpb));
+    const int64_t C = a0.s.C;
+    const bool two = st2 != nullptr && C >= kRamTwoStreamMin;
+    const int64_t c1 = two ? (C / 2 + 63) / 64 * 64 : C;      // 64-aligned: whole accept words and eval tiles
+    struct Half {
+        int64_t first, count;
+        hipStream_t st;
+    };
+    const Half H[2] = {{0, c1, st}, {c1, C - c1, st2}};
+    const int nh = two ? 2 : 1;
+    hipError_t e = hipSuccess;
+    if (two) {
+        e = hipEventRecord(ev_fork, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st2, ev_fork, 0);
+        if (e != hipSuccess) return e;
+    }
     KernelArgs a = a0;
+    a.s.nsteps = 1;
     GlmRamBufs b = b0;
     b.lpp = lpp;
-    a.s.nsteps = 1;
-    glm_ram_prop<P><<<grid, kBlock, 0, st>>>(a, b);
-    hipError_t e = hipGetLastError();
+    for (int h = 0; h < nh && e == hipSuccess; ++h) {
+        b.c0 = H[h].first;
+        glm_ram_prop<P><<<(unsigned)((H[h].count + cpb - 1) / cpb), kBlock, 0, H[h].st>>>(a, b);
+        e = hipGetLastError();
+    }
     for (int t = 0; t < a0.s.nsteps && e == hipSuccess; ++t) {
         a.s.step_begin = a0.s.step_begin + t;
-        e = mcmc_launch_glm_eval(a, b.xprop, lpp, nullptr, 0, st);           // the log-target at xprop
-        if (e != hipSuccess) break;
-        if (t + 1 < a0.s.nsteps) glm_ram_update<P, true><<<grid, kBlock, 0, st>>>(a, b);
-        else glm_ram_update<P, false><<<grid, kBlock, 0, st>>>(a, b);
-        e = hipGetLastError();
+        for (int h = 0; h < nh && e == hipSuccess; ++h) {
+            KernelArgs ae = a;                                 // the half's chains for the eval kernel
+            ae.s.C = H[h].count;
+            ae.s.order = nullptr;                              // identity (no trajectory order for RAM)
+            e = mcmc_launch_glm_eval(ae, b.xprop + H[h].first, lpp + H[h].first, nullptr, 0, H[h].st);
+            if (e != hipSuccess) break;
+            b.c0 = H[h].first;
+            const dim3 grid((unsigned)((H[h].count + cpb - 1) / cpb));
+            if (t + 1 < a0.s.nsteps) glm_ram_update<P, true><<<grid, kBlock, 0, H[h].st>>>(a, b);
+            else glm_ram_update<P, false><<<grid, kBlock, 0, H[h].st>>>(a, b);
+            e = hipGetLastError();
+        }
+    }
+    if (two) {
+        hipError_t j = hipEventRecord(ev_join, st2);
+        if (j == hipSuccess) j = hipStreamWaitEvent(st, ev_join, 0);
+        if (e == hipSuccess) e = j;
     }
     return e;
 }
@@ -213,20 +254,20 @@ static hipError_t glm_ram_wave_g(const KernelArgs& a0, const GlmRamBufs& b0, dou
 int64_t mcmc_glm_ram_wave_ustride(int d) { return d <= 256 ? 256 : d <= 512 ? 512 : 1024; }
 
 hipError_t mcmc_launch_glm_ram_wave(const mcmc::KernelArgs& a, double* u, double* nz, double* xprop, double* lpp,
-                                    hipStream_t st) {
+                                    hipStream_t st, hipStream_t st2, hipEvent_t ev_fork, hipEvent_t ev_join) {
     using namespace mcmc;
-    const GlmRamBufs b{u, nz, xprop, nullptr, mcmc_glm_ram_wave_ustride(a.s.d)};
+    const GlmRamBufs b{u, nz, xprop, nullptr, mcmc_glm_ram_wave_ustride(a.s.d), 0};
     if (a.s.d <= 256) {                                       // two chains a wave (32 lanes each, 128 G rows)
         const int g = a.s.d <= 128 ? 1 : 2;
         mcmc_note_step_kernel("glm_ram_update<GlmHalfWaveChain<%d>, true>", g);
-        return g == 1 ? glm_ram_wave_g<GlmHalfWaveChain<1>>(a, b, lpp, st)
-                      : glm_ram_wave_g<GlmHalfWaveChain<2>>(a, b, lpp, st);
+        return g == 1 ? glm_ram_wave_g<GlmHalfWaveChain<1>>(a, b, lpp, st, st2, ev_fork, ev_join)
+                      : glm_ram_wave_g<GlmHalfWaveChain<2>>(a, b, lpp, st, st2, ev_fork, ev_join);
     }
     const int g = wpc_nb_for(a.s.d);
     mcmc_note_step_kernel("glm_ram_update<GlmWaveChain<%d>, true>", g);
     switch (g) {
-        case 2: return glm_ram_wave_g<GlmWaveChain<2>>(a, b, lpp, st);
-        case 4: return glm_ram_wave_g<GlmWaveChain<4>>(a, b, lpp, st);
+        case 2: return glm_ram_wave_g<GlmWaveChain<2>>(a, b, lpp, st, st2, ev_fork, ev_join);
+        case 4: return glm_ram_wave_g<GlmWaveChain<4>>(a, b, lpp, st, st2, ev_fork, ev_join);
         default: return hipErrorInvalidValue;
     }
 }

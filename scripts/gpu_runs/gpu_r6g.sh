@@ -1,5 +1,5 @@
-# round 6, call G: glm_mala1ws with the proposal split between the M and V waves, batched normals, global (not flat)
-# state loads: parity, config-3 bench, phase stamps
+# round 6, call G: glm_mala1ws (proposal split, batched normals, unit prior, row 3 of each tile in the M wave,
+# kept rows only on kept steps): parity, config-3 bench, phase stamps
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r6g

@@ -465,6 +465,31 @@ def test_logistic_out_of_support_rejects(gpu):
     assert_parity(ch, s, g, acc, "rwm")
 
 
+@pytest.mark.parametrize("obs", [3, 12, 15])
+def test_logistic_mala_minus_inf_rule_each_row(gpu, obs):
+    """The reference's -Inf (p rounds to 1 with y = 0) triggered by one observation in row obs // 4 of the 16-
+    observation tile: glm_mala1ws splits a tile's rows between its two waves (row 3 in the M wave, round 6), whose
+    bounds combine after the tile loop; samples, gradients and accept bits bitwise against the oracle."""
+    rng = np.random.default_rng(40 + obs)
+    d, n = 8, 20
+    X = np.hstack([np.ones((n, 1)), rng.normal(size=(n, d - 1)) * 0.3])
+    X[obs] *= 100.0                                           # 400: every proposal rejected (oracle), 100: mixed
+    Y = (rng.random(n) < 0.5).astype(float)
+    Y[obs] = 0.0
+    m = mc.model(mc.LogisticRegression(X, Y), vars=np.zeros(d), gradient=True)
+    r = mc.SerialMC(steps=12, burnin=0)
+    ch = mc.run((m * mc.MALA(0.02) * r).batch(96, seed=9))
+    assert ch.task.step_kernel.startswith("glm_mala1ws")
+    oc = orc.OracleChains(m, mc.MALA(0.02), nchains=96, seed=9)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(ch, s_ref, g_ref, acc_ref, "mala")
+    assert np.array_equal(ch._gradients.view(np.uint64), g_ref.view(np.uint64))
+    a = ch.diagnostics["accept"]
+    assert 0 < a.mean() < 1                                   # both outcomes, the rejections by the -Inf rule
+    eta = np.einsum("j,sjc->sc", X[obs], s_ref)
+    assert eta.max() < 36.8 and np.abs(eta).max() > 100       # kept states stay below the rule's p == 1 edge
+
+
 @pytest.mark.parametrize("kind", ["logistic", "probit"])
 def test_covariates_that_can_overflow_to_nan_are_refused(gpu, kind):
     """X vars overflowing with mixed signs gives a NaN eta, which the reference's LLAcc turns into -Inf; the kernels
@@ -664,6 +689,43 @@ def test_glm_ram_wave_parity(gpu, kind, d):
     c2 = mc.run(chain)
     s2, _, a2 = oc.run(r)
     assert_parity(c2, s2, None, a2, "ram")
+    _assert_ram_factor(task, oc, d)
+
+
+@pytest.mark.parametrize("kind,d,sampler", [("logistic", 6, "mala"), ("linear", 300, "rwm")])
+def test_glm_state_rows_past_d_at_large_batch(gpu, kind, d, sampler):
+    """The regression kernels load the state unconditionally and zero the slots past d (round 6); such a slot reads
+    the chain's row 0, never the lane's own row, which lies past the d state rows when d is not a multiple of the
+    slice geometry (d = 6: rows 8 and 12 of glm_mala1ws's lanes; d = 300: rows 300..511 of the eval kernel's).  At
+    20 000 chains those rows would be megabytes past the state buffer; samples bitwise against the oracle."""
+    m = _glm_model(kind, d, n=40)
+    smp = mc.MALA(0.002) if sampler == "mala" else mc.RWM(0.05)
+    C = 20000
+    r = mc.SerialMC(steps=3, burnin=0)
+    task = (m * smp * r).batch(C, seed=3 + d)
+    chain = mc.run(task)
+    oc = orc.OracleChains(m, smp, nchains=C, seed=3 + d)
+    s_ref, g_ref, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, g_ref if sampler == "mala" else None, acc_ref, sampler)
+
+
+@pytest.mark.parametrize("kind,d", [("linear", 64), ("logistic", 300)])
+def test_glm_ram_wave_two_streams(gpu, kind, d):
+    """At C >= 8192 chains glm_ram_wave runs the batch as two halves on two streams (the eval kernel of one beside
+    the factor update of the other, round 6); the split is invisible: samples, accept bits, the final state and
+    every factor bitwise against the oracle, the second half's tail wave half-live (8293 chains)."""
+    m = _glm_model(kind, d, n=24)
+    C = 8293
+    r = mc.SerialMC(steps=4, burnin=1, thinning=1)
+    sc = 0.1 / np.sqrt(d)
+    task = (m * mc.RAM(sc, 0.3) * r).batch(C, seed=7 + d, steps_per_launch=2)
+    chain = mc.run(task)
+    assert task.step_kernel.startswith("glm_ram_update<"), task.step_kernel
+    oc = orc.OracleChains(m, mc.RAM(sc, 0.3), nchains=C, seed=7 + d)
+    s_ref, _, acc_ref = oc.run(r)
+    assert_parity(chain, s_ref, None, acc_ref, "ram")
+    assert np.array_equal(chain.final_x, oc.x) and np.array_equal(chain.final_lp, oc.lp)
+    assert task.evals == int(oc.n_evals.sum())
     _assert_ram_factor(task, oc, d)
 
 
