@@ -1319,7 +1319,7 @@ __device__ __forceinline__ void normals_batch(const u32x4 (&w)[NB], double (&z)[
 // there), so the results are glm_mala1's bit for bit and orc_glm_eval restates them.
 // LDS (doubles; XS = glm_tile_doubles(16 NM), X rows then Y): X slots 0, 1 | region R: X slots 2, 3, eta [2][4][64][4], r [2][4][64][4],
 // which overlays the proposal [4 waves][4 NM][64] of the proposal phase | Y [4][16] | the logistic term's table
-// (kSoftplusTab) | qf, lik [2][4][16] | M's partial qf [4][64] | row 3's term [2][4][64] and bound [4][64] (logistic).
+// (kSoftplusTab) | qf, lik [2][4][16] | M's partial qf [4][64].
 template <int NM>
 __host__ __device__ constexpr int glm_ws_region(int XS) {
     return (2 * XS + 4096) > (4 * 4 * NM * 64) ? (2 * XS + 4096) : (4 * 4 * NM * 64);
@@ -1327,7 +1327,7 @@ __host__ __device__ constexpr int glm_ws_region(int XS) {
 __host__ __device__ inline size_t glm_ws_lds_doubles(int nm) {
     const int XS = glm_tile_doubles(16 * nm);
     const int R = (2 * XS + 4096) > (4 * 4 * nm * 64) ? (2 * XS + 4096) : (4 * 4 * nm * 64);
-    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16 + 4 * 64 + 512 + 256)
+    return (size_t)(2 * XS + R + 4 * 16 + SP_NROWS * 10 + 2 * 4 * 16 + 4 * 64)
 #ifdef GLM_WS_STAMP
            + 512                                               // the phase stamps (dev build, scripts/ws_stamps.py)
 #endif
@@ -1398,10 +1398,8 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     double* const qfl = ltabp + SP_NROWS * 10;                 // qf [4][16], then lik [4][16]
     double* const likl = qfl + 64;
     double* const qpart = likl + 64;                           // M's partial qf per lane [4 tiles][64] (proposal phase)
-    double* const T3 = qpart + 256;                            // logistic: row 3's term [2][4 tiles][64] (M -> V)
-    double* const U3 = T3 + 512;                               // ... and the M wave's bound max [4 tiles][64]
 #ifdef GLM_WS_STAMP
-    unsigned* const wst = reinterpret_cast<unsigned*>(U3 + 256);
+    unsigned* const wst = reinterpret_cast<unsigned*>(qpart + 256);
 #endif
     auto xslot = [&](int64_t tt) -> double* { const int b = (int)(tt & 3); return b < 2 ? Xs + b * XS : R + (b - 2) * XS; };
     const Stream rs{s.key0, s.key1};
@@ -1539,9 +1537,8 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         }
         return e;
     };
-    auto g_of = [&](int64_t tt, double r3) {                   // G += X_tt^T r_tt (glm_eval1_tiles' G product)
-        f64x4 rv = Rq[256 * (tt & 1)];
-        if (logi) rv[3] = r3;                                  // row 3's weight: the M wave's own (logistic)
+    auto g_of = [&](int64_t tt) {                              // G += X_tt^T r_tt (glm_eval1_tiles' G product)
+        const f64x4 rv = Rq[256 * (tt & 1)];
         const double* gcol = xslot(tt) + p.q * S + 4 * (p.cl & 3) + (p.cl >> 2);
         double ga[NM];
 #pragma unroll
@@ -1573,46 +1570,17 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
     // one loop per role, each with one barrier per tile (the same count): the roles' loop invariants (the V waves'
     // polynomial constants, the M waves' operand addresses) stay out of each other's register pressure
     double lik_part = 0.0;
-    double g3 = 0.0;                                           // M: the last tile's row-3 weight
     double ubnd = -__builtin_inf();                            // logistic: max of u + b over the lane's observations
-    // logistic: the M wave takes row 3 of each tile's elementwise work (the V wave rows 0..2).  The M wave has waited
-    // ~1 600 cycles a tile at the barrier for the V wave's terms, which ran mostly after the MFMAs stopped (the two do
-    // not co-issue on a SIMD); with two waves on the elementwise work its latency overlaps.  Row 3's term crosses to
-    // the V wave through LDS (T3, by tile parity) and is added first in the next tile, so the lane's terms still sum
-    // in (t, r) order; its weight stays in the M wave for G; the bound's max is combined after the loop.
     if (!vwave) {
-        f64x4 eta_t = Eq[0];                                   // eta_0, from the registers it was stored from
-        double rv3 = 0.0;                                      // row 3's weight of tile t - 1 (G_{t-1})
-        double ub3 = -__builtin_inf();
         for (int64_t t = 0; t < ntiles; ++t) {
             WS_STAMP(0);
-            f64x4 eta_n = eta_t;
-            if (t + 1 < ntiles) {
-                eta_n = eta_of(t + 1);
-                Eq[256 * ((t + 1) & 1)] = eta_n;
-            }
+            if (t + 1 < ntiles) Eq[256 * ((t + 1) & 1)] = eta_of(t + 1);
             WS_STAMP(1);
-            if (t >= 1) g_of(t - 1, rv3);
+            if (t >= 1) g_of(t - 1);
             WS_STAMP(2);
-            if (logi) {
-                const double* X0 = xslot(t);
-                const double w3 = X0[YO + p.q + 12];
-                LogiState E;
-                det_logi_s1(eta_t[3], w3, E, sptab);
-                ub3 = __builtin_fmax(ub3, E.u + X0[BO + p.q + 12]);               // the reference's -Inf
-                det_logi_s2(E);
-                double term3, r3;
-                det_logi_fin(E, w3, term3, r3);
-                const bool in = t < nfull || t * 16 + p.q + 12 < M.n;
-                rv3 = in ? r3 : 0.0;
-                T3[256 * (t & 1) + p.tile * 64 + p.lane] = term3;
-                if (t + 1 == ntiles) U3[p.tile * 64 + p.lane] = ub3;
-            }
-            eta_t = eta_n;
             __syncthreads();
             WS_STAMP(3);
         }
-        g3 = rv3;
     } else {
         for (int64_t t = 0; t < ntiles; ++t) {
             WS_STAMP(0);
@@ -1627,34 +1595,23 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) y[r] = LY[p.q + 4 * r];
             if (logi) {
-                // row 3 of tile t - 1 (the M wave's), before this tile's rows: the (t, r) order
-                if (t >= 1 && (t - 1 < nfull || (t - 1) * 16 + p.q + 12 < M.n))
-                    lik_part = lik_part + T3[256 * ((t - 1) & 1) + p.tile * 64 + p.lane];
-                // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111);
-                // rows 0..2 here, row 3 in the M wave
+                // prob = 1/(1+exp(-X*vars)); Y ~ Bernoulli(prob); its eta-derivative (MCMCDerivRules.jl:111)
                 const double* LB = xslot(t) + BO;
-                {
+                // two rows at a time: four rows' coefficient rows in flight at once spill the wave's registers
+#pragma unroll
+                for (int h = 0; h < 4; h += 2) {
                     LogiState E[2];
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
-                        det_logi_s1(eta[r], y[r], E[r], sptab);
-                        ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * r]);      // the reference's -Inf
+                        det_logi_s1(eta[h + r], y[h + r], E[r], sptab);
+                        ubnd = __builtin_fmax(ubnd, E[r].u + LB[p.q + 4 * (h + r)]);   // the reference's -Inf
                     }
 #pragma unroll
                     for (int r = 0; r < 2; ++r) det_logi_s2(E[r]);
 #pragma unroll
-                    for (int r = 0; r < 2; ++r) det_logi_fin(E[r], y[r], term[r], rv[r]);
+                    for (int r = 0; r < 2; ++r) det_logi_fin(E[r], y[h + r], term[h + r], rv[h + r]);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                {
-                    LogiState E;
-                    det_logi_s1(eta[2], y[2], E, sptab);
-                    ubnd = __builtin_fmax(ubnd, E.u + LB[p.q + 8]);
-                    det_logi_s2(E);
-                    det_logi_fin(E, y[2], term[2], rv[2]);
-                }
-                term[3] = 0.0;
-                rv[3] = 0.0;
             } else if (M.kind == MK_PROBIT) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) glm_probit_obs(eta[r], y[r], term[r], rv[r]);
@@ -1667,15 +1624,12 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
                     rv[r] = resid * is2n;
                 }
             }
-            const int nr = logi ? 3 : 4;                                           // logistic: row 3 in the M wave
             if (t < nfull) {                                                       // uniform: no padded observation
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (r < nr) lik_part = lik_part + term[r];                     // the lane's terms in (t, r) order
+                for (int r = 0; r < 4; ++r) lik_part = lik_part + term[r];         // the lane's terms in (t, r) order
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    if (r >= nr) continue;
                     const bool in = t * 16 + p.q + 4 * r < M.n;
                     lik_part = in ? lik_part + term[r] : lik_part;
                     rv[r] = in ? rv[r] : 0.0;
@@ -1694,15 +1648,10 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         for (int j = p.lane; j < 128; j += 64) (&g_ws_stamps[blockIdx.x][wv][0][0])[j] = wst[wv * 128 + j];
 #endif
     if (vwave) {
-        if (logi) {                                            // the last tile's row 3 and the M wave's bound
-            const int64_t tl = ntiles - 1;
-            if (tl < nfull || tl * 16 + p.q + 12 < M.n) lik_part = lik_part + T3[256 * (tl & 1) + p.tile * 64 + p.lane];
-            ubnd = __builtin_fmax(ubnd, U3[p.tile * 64 + p.lane]);
-        }
         const double lik = glm_sum(a, p, GlmLds{}, logi && ubnd >= 0.0 ? -__builtin_inf() : lik_part);
         if (p.q == 0) likl[p.tile * 16 + p.cl] = lik;
     } else {
-        g_of(ntiles - 1, g3);
+        g_of(ntiles - 1);
     }
     __syncthreads();
     WS_WG(5);

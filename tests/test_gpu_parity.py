@@ -467,9 +467,9 @@ def test_logistic_out_of_support_rejects(gpu):
 
 @pytest.mark.parametrize("obs", [3, 12, 15])
 def test_logistic_mala_minus_inf_rule_each_row(gpu, obs):
-    """The reference's -Inf (p rounds to 1 with y = 0) triggered by one observation in row obs // 4 of the 16-
-    observation tile: glm_mala1ws splits a tile's rows between its two waves (row 3 in the M wave, round 6), whose
-    bounds combine after the tile loop; samples, gradients and accept bits bitwise against the oracle."""
+    """The reference's -Inf (p rounds to 1 with y = 0) triggered by one observation in row obs // 4 of a 16-
+    observation tile (obs 3, 12: the first tile's rows 0 and 3; 15: its last lane quarter), in glm_mala1ws' V wave;
+    samples, gradients and accept bits bitwise against the oracle, both outcomes present."""
     rng = np.random.default_rng(40 + obs)
     d, n = 8, 20
     X = np.hstack([np.ones((n, 1)), rng.normal(size=(n, d - 1)) * 0.3])
