@@ -53,6 +53,11 @@ __device__ __forceinline__ double ram_bcast(double v, int j) {
 // counts the memory operations exactly, and the wait for column k + 1's prefetched entries does not also wait
 // for column k's stores (a masked, branched access makes it wait for everything: vmcnt(0)).
 constexpr uint32_t kRamOob = 0xfffffff0u;
+// columns of the factor in flight in ram_wave_update (1: the next column's loads issued before this one's update; 2:
+// the next two)
+#ifndef RAM_WAVE_PF
+#define RAM_WAVE_PF 2
+#endif
 __device__ __forceinline__ double ram_wload_m(ram_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
@@ -119,12 +124,18 @@ __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, ui
 #pragma unroll
         for (int s = 0; s < NC; ++s) un[s] = 0.0;
     }
-    double l0[NC];
+    // column k's entries l0, the next RAM_WAVE_PF - 1 columns' loads in flight (the update is a chain over the
+    // columns; the loads are not: more of them in flight is more of the factor's bandwidth)
+    double l0[NC], l1[NC], lp2[NC];
     ram_wave_load_col<NC, L>(Ss, vo, lane, d, 0, l0);
+    if (RAM_WAVE_PF > 1 && d > 1) ram_wave_load_col<NC, L>(Ss, vo, lane, d, 1, l1);
     ram_wave_columns<NC, L>(d, [&](int k, int j, int ks) {
         const uint32_t base = vo + (uint32_t)(ram_wave_colstart(k, d) - k) * 8u;
-        double l1[NC];
-        if (k + 1 < d) ram_wave_load_col<NC, L>(Ss, vo, lane, d, k + 1, l1);
+        if (RAM_WAVE_PF > 1) {
+            if (k + 2 < d) ram_wave_load_col<NC, L>(Ss, vo, lane, d, k + 2, lp2);
+        } else {
+            if (k + 1 < d) ram_wave_load_col<NC, L>(Ss, vo, lane, d, k + 1, l1);
+        }
         const double zk = NEXT ? ram_bcast<L>(zn[ks], j) : 0.0;
         const double lkk = ram_bcast<L>(l0[ks], j);
         const double xk = ram_bcast<L>(u[ks], j);
@@ -150,7 +161,10 @@ __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, ui
             u[s] = below ? u1 : u[s];
         }
 #pragma unroll
-        for (int s = 0; s < NC; ++s) l0[s] = l1[s];
+        for (int s = 0; s < NC; ++s) {
+            l0[s] = l1[s];
+            if (RAM_WAVE_PF > 1) l1[s] = lp2[s];
+        }
     });
 }
 
