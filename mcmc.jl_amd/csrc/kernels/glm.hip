@@ -460,15 +460,16 @@ __device__ __forceinline__ void glm_dma_tile(const double* img, double* buf) {
 #pragma unroll
     for (int j = 0; j < glm_dma_pieces_per_wave<TS>(); ++j) glm_dma_piece<TS>(img, buf, j);
 }
-// GLM_DMA_SPREAD (default 0): the next tile's pieces issued between the eta MFMAs (one after every second MFMA)
-// instead of all before the eta operand reads
+// GLM_DMA_SPREAD (default 2; 0: off): the next tile's pieces issued between the eta MFMAs, one after every
+// GLM_DMA_SPREAD-th MFMA, instead of all before the eta operand reads (round 6, config 5: 0.584 -> 0.605 of the fp64
+// spec, profiles/r06_ab_glm.md)
 // GLM_ETA_LA (default 8): how many eta A-operand reads run ahead of their MFMA in the 128-wide slices (NM = 8; the
 // 64-wide slices read all 16 before the first MFMA)
 #ifndef GLM_ETA_LA
 #define GLM_ETA_LA 8
 #endif
 #ifndef GLM_DMA_SPREAD
-#define GLM_DMA_SPREAD 0
+#define GLM_DMA_SPREAD 2
 #endif
 // a workgroup barrier for LDS data written by ds_write (lgkmcnt) that leaves LDS-DMAs in flight: __syncthreads()
 // would also wait vmcnt(0), draining the next tile's copy (cdna_hip_programming.md §5, pipelining across barriers)
@@ -574,14 +575,16 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             for (int m = 0; m < KM; ++m) {
                 if (m + kLA < KM) av[m + kLA] = xrow[glm_eta_off(m + kLA)];
                 eta = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], x[m], eta, 0, 0, 0);
-                if (GLM_DMA_SPREAD && !kOneBuf && (m & 1) && (m >> 1) < glm_dma_pieces_per_wave<XS>()) {
-                    if (more) glm_dma_piece<XS>(nimg, nbuf, m >> 1);
+                constexpr int SP = GLM_DMA_SPREAD > 0 ? GLM_DMA_SPREAD : 1;
+                if (GLM_DMA_SPREAD && !kOneBuf && m % SP == SP - 1 && m / SP < glm_dma_pieces_per_wave<XS>()) {
+                    if (more) glm_dma_piece<XS>(nimg, nbuf, m / SP);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
             if (GLM_DMA_SPREAD && !kOneBuf && more) {
+                constexpr int SP = GLM_DMA_SPREAD > 0 ? GLM_DMA_SPREAD : 1;
 #pragma unroll
-                for (int j = KM / 2; j < glm_dma_pieces_per_wave<XS>(); ++j) glm_dma_piece<XS>(nimg, nbuf, j);
+                for (int j = KM / SP; j < glm_dma_pieces_per_wave<XS>(); ++j) glm_dma_piece<XS>(nimg, nbuf, j);
             }
         }
         // Elementwise part, split over the slice waves: wave slice s owns observation rows r in
