@@ -67,6 +67,11 @@ constexpr bool kGlmGFence = GLM_GFENCE != 0;
 #ifndef GLM_WS_LA
 #define GLM_WS_LA 4
 #endif
+// GLM_WS_DMA (default 1): glm_mala1ws's V waves stage the X ring's tile t+2 by LDS-DMA (global_load_lds, no
+// registers, no ds_write) instead of through registers
+#ifndef GLM_WS_DMA
+#define GLM_WS_DMA 1
+#endif
 // NM (template parameter) = DS/16 in {1, 2, 4, 8}: the lane owns NS = 4*NM coordinates.
 
 struct GlmShape {
@@ -459,6 +464,22 @@ template <int TS>
 __device__ __forceinline__ void glm_dma_tile(const double* img, double* buf) {
 #pragma unroll
     for (int j = 0; j < glm_dma_pieces_per_wave<TS>(); ++j) glm_dma_piece<TS>(img, buf, j);
+}
+// tile image img -> LDS buffer buf by the NWV waves of one role (w: the wave's index among them, wave-uniform),
+// pieces w, w + NWV, ... (glm_mala1ws: the V waves stage the X ring)
+template <int TS, int NWV>
+__device__ __forceinline__ void glm_dma_tile_w(const double* img, double* buf, int w) {
+    constexpr int kPieces = TS / 128;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < (kPieces + NWV - 1) / NWV; ++j) {
+        const int c = w + NWV * j;
+        if (c < kPieces) {
+            const double* src = img + c * 128 + 2 * lane;
+            const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(uintptr_t)buf + (uint32_t)c * 1024u));
+            asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src), "{m0}"(lds) : "memory");
+        }
+    }
 }
 // GLM_DMA_SPREAD (default 2; 0: off): the next tile's pieces issued between the eta MFMAs, one after every
 // GLM_DMA_SPREAD-th MFMA, instead of all before the eta operand reads (round 6, config 5: 0.584 -> 0.605 of the fp64
@@ -1520,7 +1541,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         qf = glm_sum(a, p, GlmLds{}, qf);
         if (p.q == 0) qfl[p.tile * 16 + p.cl] = qf;
         WS_WG2(2);
-        if (ntiles > 2) load_tile(2);
+        if (!GLM_WS_DMA && ntiles > 2) load_tile(2);
     }
     __syncthreads();                                           // the proposal area is free from here on
     WS_WG(2);
@@ -1588,8 +1609,12 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
         for (int64_t t = 0; t < ntiles; ++t) {
             WS_STAMP(0);
             if (t + 2 < ntiles) {                              // slot (t+2) % 4 held tile t-2: read before the last barrier
-                store_tile(t + 2);
-                if (t + 3 < ntiles) load_tile(t + 3);
+                if (GLM_WS_DMA) {
+                    glm_dma_tile_w<XS, 4>(M.X + (size_t)(t + 2) * XS, xslot(t + 2), __builtin_amdgcn_readfirstlane(wv - 4));
+                } else {
+                    store_tile(t + 2);
+                    if (t + 3 < ntiles) load_tile(t + 3);
+                }
             }
             WS_STAMP(1);
             const f64x4 eta = Eq[256 * (t & 1)];
@@ -1641,6 +1666,7 @@ __global__ __launch_bounds__(512) void glm_mala1ws(GlmArgs a) {
             WS_STAMP(2);
             Rq[256 * (t & 1)] = f64x4{rv[0], rv[1], rv[2], rv[3]};
             WS_STAMP(3);
+            if (GLM_WS_DMA) glm_dma_wait();                    // tile t+2 landed (the asm loads are not counted)
             __syncthreads();
             WS_STAMP(4);
         }
