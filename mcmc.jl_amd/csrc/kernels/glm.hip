@@ -2123,7 +2123,9 @@ static hipError_t glm_step_nm(const mcmc::GlmArgs& a, size_t lds, dim3 grid, hip
     switch (a.sa.kind) {
         case SK_RWM: mcmc_note_step_kernel("glm_rwm<%d, %d>", NM, NW); break;
         case SK_MALA:
-            if (NW == 1) mcmc_note_step_kernel(GLM_MALA1_WS ? "glm_mala1ws<%d>" : "glm_mala1<%d>", NM);
+            if (NW == 1 && GLM_MALA1_WS && NM == 8 && a.m.prior_sigma == 1.0)
+                mcmc_note_step_kernel("glm_mala1ws<%d, true>", NM);          // the unit-prior instance
+            else if (NW == 1) mcmc_note_step_kernel(GLM_MALA1_WS ? "glm_mala1ws<%d>" : "glm_mala1<%d>", NM);
             else mcmc_note_step_kernel("glm_mala<%d, %d>", NM, NW);
             break;
         case SK_HMC: mcmc_note_step_kernel("glm_hmc<%d, %d, false>", NM, NW); break;

@@ -201,7 +201,7 @@ def test_config3_logistic_mala_instance(gpu, tuned, link_sign, prior):
     r = mc.SerialMC(steps=5, burnin=1, thinning=2)
     t = (m * smp() * r).batch(200, seed=31)
     chain = mc.run(t)
-    assert t.step_kernel == "glm_mala1ws<8>"
+    assert t.step_kernel == ("glm_mala1ws<8, true>" if prior == 1.0 else "glm_mala1ws<8>")
     oc = orc.OracleChains(m, smp(), nchains=200, seed=31)
     s_ref, g_ref, acc_ref = oc.run(r)
     _check(chain, s_ref, acc_ref)
