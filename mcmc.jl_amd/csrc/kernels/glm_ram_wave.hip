@@ -17,12 +17,6 @@
 
 namespace mcmc {
 
-// waves per SIMD the update kernel is compiled for (the factor update is latency-bound on its column chain: more
-// waves, more columns in flight)
-#ifndef GLM_RAM_WAVES
-#define GLM_RAM_WAVES 4
-#endif
-
 // A wave-per-chain policy's coordinate layout (lane l of the chain's L, slot 4 g + e <-> coordinate 4 (l + L g) + e)
 // over the regression state [d][ld] and the C ABI's kept layout [nkept][d][C]; B = WaveChain (L = 64) or
 // HalfWaveChain (L = 32, two chains a wave)
@@ -131,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void glm_ram_prop(KernelArgs a, GlmRamBufs 
 
 // step i: accept (RAM.jl:62-71), kept rows, the factor update (RAM.jl:74-78); NEXT: step i + 1's u, |rvec|^2, xprop
 template <class P, bool NEXT>
-__global__ __launch_bounds__(kBlock, GLM_RAM_WAVES) void glm_ram_update(KernelArgs a, GlmRamBufs b) {
+__global__ __launch_bounds__(kBlock) void glm_ram_update(KernelArgs a, GlmRamBufs b) {
     constexpr int NC = P::NC, L = P::L, CPW = P::CPW;
     const StepArgs& s = a.s;
     const SamplerArgs& sa = a.sa;
