@@ -196,6 +196,12 @@ def step_kernel_src_hash():
     return h.hexdigest()[:16]
 
 
+def kernel_src_hash(kname):
+    """The source hash a profile of this kernel instance is keyed by: the regression kernels (glm*) are built from
+    glm_src_hash's sources, every other step kernel from step_kernel_src_hash's."""
+    return glm_src_hash() if _norm_kernel(kname).startswith("glm") else step_kernel_src_hash()
+
+
 def measured_valu(kname, wkey):
     """VALU issue cost of the step kernel per chain-step (SQ_ACTIVE_INST_VALU quad-cycles / chain-steps of the
     timed dispatch) and its measured VALU-busy fraction, from a committed rocprofv3 PMC run of this kernel
@@ -205,7 +211,7 @@ def measured_valu(kname, wkey):
     p = os.path.join(ROOT, "profiles", "valu.json")
     if not os.path.exists(p):
         return None
-    h = step_kernel_src_hash()
+    h = kernel_src_hash(kname)
     for k, e in json.load(open(p)).items():
         if (_norm_kernel(e.get("kernel", k)) == _norm_kernel(kname) and e.get("src_hash") == h
                 and e.get("workload_key") == wkey):
@@ -744,7 +750,7 @@ def main():
         roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": achieved / F64_MFMA_PEAK_TFS, "traffic": traffic, "traffic_detail": tdet, "kernel": kname,
                 "launches": launches, "avg_launch_ms": avg_launch_s * 1e3, "flop_per_eval": flop_per_eval,
-                "evals_per_launch": evals / launches,
+                "evals_per_launch": evals / launches, "units_per_launch": C * K / launches,
                 "note": "units = log-target+gradient evaluations (leapfrogs for HMC/HMCDA, counted on the "
                         "device); 4 n d fp64 flop each (SURVEY.md §8(d))"}
         if args.sampler == "ram":
@@ -767,6 +773,26 @@ def main():
                         "bytes_per_unit": hbm["bytes_per_unit"], "mfma": mf, "note": hbm["note"]}
             else:
                 roof["hbm"] = hbm
+        vm = measured_valu(kname, wkey)
+        if vm is not None and args.sampler != "ram":
+            # the small regression targets (d <= 16: one MFMA covers a 16-chain tile's contraction): the per-step
+            # RNG and elementwise work issue on the VALU, which the fp64 MFMAs also occupy; the
+            # VALU issue fraction of a committed PMC profile names the bound when it is the larger
+            cyc = 4.0 * vm["valu_quadcycles_per_chain_step"]
+            ach = cyc * C * K / launches / avg_launch_s / 1e12
+            vroof = {"achieved": ach, "peak": VALU_PEAK_TCYC, "unit": "T VALU-issue-cycles/s",
+                     "frac": ach / VALU_PEAK_TCYC, "valu_cycles_per_unit": cyc, "valu_busy_measured": vm["valu_busy"],
+                     "clock_ghz_measured": vm["clock_ghz"], "valu_source": vm["source"],
+                     "note": "units = chain-steps; SQ_ACTIVE_INST_VALU of a committed PMC profile (fp64 MFMAs "
+                             "included: they issue on the VALU)"}
+            if vroof["frac"] > roof["frac"]:
+                mf = dict(roof)
+                for k in ("kernel", "launches", "avg_launch_ms", "traffic", "traffic_detail"):
+                    mf.pop(k, None)
+                roof = dict(vroof, bound="valu", traffic=traffic, kernel=kname, launches=launches,
+                            avg_launch_ms=avg_launch_s * 1e3, units_per_launch=C * K / launches, mfma=mf)
+            else:
+                roof["valu"] = vroof
         fm = measured_fp64(kname, wkey)
         if fm is not None:                                            # MFMA + VALU fp64 on the shared datapath
             per_eval = fm["mfma_flop_per_eval"] + fm["valu_fp64_flop_per_eval"]

@@ -72,8 +72,8 @@ for c in sorted(v):
     L.append(f"| {c} | {v[c]:.6g} | {v[c] / waves / steps:.2f} |")
 open(os.path.join(root, "profiles", f"{tag}.md"), "w").write("\n".join(L) + "\n")
 sys.path.insert(0, root)
-from bench import step_kernel_src_hash  # noqa: E402
-entry["src_hash"] = step_kernel_src_hash()   # the sources this profile measured (bench.py ignores other hashes)
+from bench import kernel_src_hash  # noqa: E402
+entry["src_hash"] = kernel_src_hash(entry.get("kernel", ""))   # the sources it measured (bench.py ignores others)
 p = os.path.join(root, "profiles", "valu.json")
 tj = json.load(open(p)) if os.path.exists(p) else {}
 tj[f"{kname}|{entry['workload_key']}"] = entry        # one entry per kernel and workload
