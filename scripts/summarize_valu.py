@@ -28,6 +28,10 @@ for d in sorted(glob.glob(os.path.join(src, "p*/"))):
     rows = [r for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))) if pat in r["Kernel_Name"]]
     if not rows:
         continue
+    # the timed launches are the kernel's full-grid dispatches (a few-chain reference run of the same instance may
+    # follow them): the last dispatch of the largest grid
+    gmax = max(int(r["Grid_Size"]) for r in rows)
+    rows = [r for r in rows if int(r["Grid_Size"]) == gmax]
     last = max(int(r["Dispatch_Id"]) for r in rows)
     for r in rows:
         if int(r["Dispatch_Id"]) == last:
