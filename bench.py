@@ -774,7 +774,7 @@ def main():
             else:
                 roof["hbm"] = hbm
         vm = measured_valu(kname, wkey)
-        if vm is not None and args.sampler != "ram":
+        if vm is not None:
             # the small regression targets (d <= 16: one MFMA covers a 16-chain tile's contraction): the per-step
             # RNG and elementwise work issue on the VALU, which the fp64 MFMAs also occupy; the
             # VALU issue fraction of a committed PMC profile names the bound when it is the larger
