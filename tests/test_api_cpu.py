@@ -209,17 +209,18 @@ def test_bench_traffic_only_from_a_profile_of_the_same_kernel():
 
 
 def test_bench_valu_roofline_profile():
-    """A VALU profile prices a run only when it was recorded from the same step-kernel sources, for the same kernel
-    instance and the same workload (steps included); every committed profile implies a VALU fraction <= 1 at its
-    own measured clock."""
+    """A VALU profile prices a run only when it was recorded from the sources of its kernel's family (the regression
+    kernels' or the other step kernels'), for the same kernel instance and the same workload (steps included); every
+    committed profile implies a VALU fraction <= 1 at its own measured clock."""
     import importlib
     import json
     bench = importlib.import_module("bench")
     prof = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
-    h = bench.step_kernel_src_hash()
+    assert bench.kernel_src_hash("glm_rwm<1, 1>") == bench.glm_src_hash()
+    assert bench.kernel_src_hash("void mcmc::lpp_rwm<4, true, IsoDot, true>(mcmc::KernelArgs)") == bench.step_kernel_src_hash()
     for k, e in prof.items():
         got = bench.measured_valu(e["kernel"], e["workload_key"])
-        assert (got is not None) == (e["src_hash"] == h)
+        assert (got is not None) == (e["src_hash"] == bench.kernel_src_hash(e["kernel"]))
         assert bench.measured_valu(e["kernel"], e["workload_key"] + "x") is None      # another workload
         assert bench.measured_valu("lpc_rwm<9,true,X,true>", e["workload_key"]) is None
         assert os.path.exists(os.path.join(ROOT, e["source"]))
