@@ -58,6 +58,10 @@ constexpr uint32_t kRamOob = 0xfffffff0u;
 #ifndef RAM_WAVE_PF
 #define RAM_WAVE_PF 2
 #endif
+// 1 (default): a column's per-slot work starts at the owner's slot (the slots before hold rows above the pivot)
+#ifndef RAM_WAVE_PRUNE
+#define RAM_WAVE_PRUNE 1
+#endif
 __device__ __forceinline__ double ram_wload_m(ram_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
@@ -102,6 +106,7 @@ __device__ __forceinline__ void ram_wave_matvec(ram_rsrc_t S, uint32_t vo, int l
         ram_wave_load_col<NC, L>(S, vo, lane, d, k, v);
 #pragma unroll
         for (int s = 0; s < NC; ++s) {
+            if (RAM_WAVE_PRUNE && s < ks) continue;            // rows L s .. L s + L - 1 < k: none takes column k
             const int q = lane + L * s;
             const double f = __builtin_fma(v[s], zk, u[s]);
             u[s] = (q >= k && q < d) ? f : u[s];
@@ -148,8 +153,11 @@ __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, ui
         const double ic = 1.0 / cc;
 #pragma unroll
         for (int s = 0; s < NC; ++s) {
-            // every slot computes; selects keep the entries outside rows k..d-1 unchanged (the same values as
-            // per-row branches: row k takes r, rows below take l)
+            // every slot from the owner's on computes (the slots before it hold rows above k: no entry of theirs
+            // changes, so they are skipped, a compile-time bound of the unrolled owner slot); selects keep the
+            // entries outside rows k..d-1 unchanged (the same values as per-row branches: row k takes r, rows below
+            // take l)
+            if (RAM_WAVE_PRUNE && s < ks) continue;
             const int q = lane + L * s;
             const bool diag = q == k, below = q > k && q < d;
             const double l = (l0[s] + sns * u[s]) * ic;
@@ -162,6 +170,7 @@ __device__ __forceinline__ void ram_wave_update(ram_rsrc_t Ss, ram_rsrc_t Sd, ui
         }
 #pragma unroll
         for (int s = 0; s < NC; ++s) {
+            if (RAM_WAVE_PRUNE && s < ks) continue;            // rows above every later column
             l0[s] = l1[s];
             if (RAM_WAVE_PF > 1) l1[s] = lp2[s];
         }
