@@ -58,8 +58,9 @@ hipError_t mcmc_seqmc_store(int64_t N, int d, const double* pars, const double* 
 // effective sample size of every (parameter, chain) series of samples [n][d][C] (stats.hip)
 hipError_t mcmc_launch_ess(const double* samples, int64_t n, int64_t d, int64_t C, int32_t vtype, int64_t maxlag,
                            int64_t batchlen, double* ess, double* var, hipStream_t st);
-// padded coordinate count of the regression kernels
+// padded coordinate count of the regression kernels; their 16-chain tiles per workgroup
 int mcmc_glm_d_pad(int d);
+int mcmc_glm_tiles_per_wg(int d);
 // the regression kernels' staged-tile image of X and Y (glm_layout.hpp): its size in doubles, and the packing
 size_t mcmc_glm_image_doubles(int d, int64_t n);
 void mcmc_glm_pack_image(int d, int64_t n, const double* X, const double* Y, const double* B, double* img);

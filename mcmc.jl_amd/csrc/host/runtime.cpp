@@ -670,6 +670,25 @@ static int glm_trajectory_order(mcmc_chains* c, hipStream_t st) {
         const bool na = std::isnan(ka), nb = std::isnan(kb);
         return na != nb ? nb : (!na && ka < kb);
     });
+    // two tiles a workgroup (d-sliced, 128 < d <= 512): the longest tile shares its workgroup with the shortest, the
+    // second longest with the second shortest, ...: the workgroup runs its longer tile's trajectory, and once the
+    // shorter tile's chains have all finished it stops computing (glm_hmc, GLM_TILE_SKIP), so the long tiles -- the
+    // dispatch's end -- run their tails with the SIMDs to themselves.  Whole 32-chain workgroups only.
+    static const bool pair_off = [] {                  // MCMCHIP_TILE_PAIR=0: sorted neighbours share (A/B)
+        const char* e = std::getenv("MCMCHIP_TILE_PAIR");
+        return e != nullptr && e[0] == '0';
+    }();
+    if (!pair_off && mcmc_glm_tiles_per_wg(c->model->args.d) == 2 && C % 32 == 0) {
+        const int64_t nt = C / 16;
+        std::vector<int32_t> paired((size_t)C);
+        for (int64_t w = 0; w < nt / 2; ++w)
+            for (int h = 0; h < 2; ++h) {
+                const int64_t src = h == 0 ? w : nt - 1 - w;             // sorted tile
+                for (int k = 0; k < 16; ++k)
+                    paired[(size_t)((2 * w + h) * 16 + k)] = c->h_order[(size_t)(src * 16 + k)];
+            }
+        c->h_order.swap(paired);
+    }
     HIP_TRY(hipMemcpyAsync(c->order_buf.p, c->h_order.data(), (size_t)C * sizeof(int32_t), hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
     return MCMC_OK;

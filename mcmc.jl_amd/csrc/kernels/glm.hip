@@ -191,6 +191,27 @@ __device__ __forceinline__ int64_t glm_max(const GlmLds& L, int64_t v, bool live
     return r;
 }
 
+// the workgroup-wide max of a per-chain integer and the max over this wave's chain tile (d-sliced geometry: at most
+// two tiles a workgroup); every wave must reach it
+__device__ __forceinline__ int64_t glm_max_tile(const GlmLds& L, int64_t v, bool live, int tile, int64_t& tmax) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        L.iscr[0] = 1;
+        L.iscr[1] = 1;
+        L.iscr[2] = 1;
+    }
+    __syncthreads();
+    if (live) {
+        atomicMax(&L.iscr[0], (int)v);
+        atomicMax(&L.iscr[1 + tile], (int)v);
+    }
+    __syncthreads();
+    const int r = L.iscr[0];
+    tmax = L.iscr[1 + tile];
+    __syncthreads();
+    return r;
+}
+
 // The lane's coordinates of the evaluation point: held in registers (XArr) or in the lane's private
 // LDS slots (XLds: slot s at b[64 s], b = L.beta + (wave * 4 NM) * 64 + lane).
 template <int NS>
@@ -207,7 +228,7 @@ struct XLds {
 // prior vars ~ Normal(0, sp) over own coordinates, the LLAcc rule, and the prior's gradient added to G.
 template <int NM, int NW, bool GRAD, class XA>
 __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
-                                          const XA& x, f64x4 (&G)[NM], double lik_part, bool& oos) {
+                                          const XA& x, f64x4 (&G)[NM], double lik_part, bool& oos, bool on = true) {
     const ModelArgs& M = a.m;
     const int d = M.d;
     const double lik = glm_sum(a, p, L, lik_part);
@@ -229,7 +250,7 @@ __device__ __forceinline__ double glm_finish(const GlmArgs& a, const GlmPos& p, 
     bad = bad || !(acc - acc == 0.0);
     oos = bad;
     if (bad) acc = -__builtin_inf();
-    if (GRAD) {
+    if (GRAD && on) {
 #pragma unroll
         for (int slot = 0; slot < (4 * NM); ++slot)
             G[slot >> 2][slot & 3] = bad ? 0.0 : (0.0 - x(slot)) / s2p + G[slot >> 2][slot & 3];
@@ -492,6 +513,11 @@ __device__ __forceinline__ void glm_dma_tile_w(const double* img, double* buf, i
 #ifndef GLM_DMA_SPREAD
 #define GLM_DMA_SPREAD 2
 #endif
+// GLM_TILE_SKIP (default 1): in glm_hmc's d-sliced trajectories a chain tile whose chains have all finished skips
+// its evaluations' MFMA and elementwise work for the rest of the workgroup's trajectory
+#ifndef GLM_TILE_SKIP
+#define GLM_TILE_SKIP 1
+#endif
 // a workgroup barrier for LDS data written by ds_write (lgkmcnt) that leaves LDS-DMAs in flight: __syncthreads()
 // would also wait vmcnt(0), draining the next tile's copy (cdna_hip_programming.md §5, pipelining across barriers)
 __device__ __forceinline__ void glm_lds_barrier() {
@@ -530,9 +556,12 @@ static __device__ unsigned g_glm_stamps[4][8][16][8];
 //     barrier; every wave reads its tile's 4 rows' weights; G += X_t^T r (NM independent accumulators)
 //     vmcnt(0) + barrier: tile t+1 has landed and tile t's buffer, part and rbuf are free again.
 // Two tiles of chains share each staged tile (reuse 32 chains per X byte from L2 / MALL).
+// on = false (wave-uniform; a chain tile whose every chain has finished its trajectory, glm_hmc): the wave takes its
+// share of the staging and every barrier, and skips its MFMAs and elementwise work; G is left as it is and the
+// returned value is not the log-target (the caller keeps its own).
 template <int NM, int NW, bool GRAD>
 __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, const GlmLds& L,
-                                        const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos) {
+                                        const double (&x)[(4 * NM)], f64x4 (&G)[NM], bool& oos, bool on = true) {
     if constexpr (NW == 1) return glm_eval1<NM, GRAD>(a, p, L, XArr<4 * NM>{x}, G, oos);
     const ModelArgs& M = a.m;
     const GlmShape& g = a.g;
@@ -546,7 +575,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
     const double sn = M.noise_sigma, s2n = sn * sn;
     const double logsn = logistic ? 0.0 : det_log(sn);
     const double isn = 1.0 / sn, is2n = 1.0 / s2n;
-    if (GRAD) {
+    if (GRAD && on) {
 #pragma unroll
         for (int T = 0; T < NM; ++T) G[T] = f64x4{0.0, 0.0, 0.0, 0.0};
     }
@@ -568,7 +597,8 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         const bool more = t + 1 < ntiles;
         const double* const nimg = M.X + (size_t)(t + 1) * XS;
         double* const nbuf = L.X + (b ^ 1) * XS;
-        if (!GLM_DMA_SPREAD && more && !kOneBuf) glm_dma_tile<XS>(nimg, nbuf);
+        // the wave's share of tile t+1's DMA: spread over its eta MFMAs (GLM_DMA_SPREAD), all here without them
+        if ((!GLM_DMA_SPREAD || !on) && more && !kOneBuf) glm_dma_tile<XS>(nimg, nbuf);
         // eta partial over this wave's coordinates: k-slice kk = 4m + e, row q <-> coord base+16m+4q+e.  Every operand
         // read is issued before the first MFMA (a scheduling fence keeps them there: left alone, the scheduler sank
         // each read next to its MFMA and the chain waited out every LDS round trip); the waitcnt pass then waits
@@ -584,7 +614,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
             for (int rr_ = 0; rr_ < RPW; ++rr_) bv[rr_] = LX[BO + p.q + 4 * ((r0 + rr_) & 3)];
         }
         f64x4 eta = f64x4{0.0, 0.0, 0.0, 0.0};
-        {
+        if (on) {
             constexpr int KM = 4 * NM;
             constexpr int kLA = NM <= 4 ? KM : GLM_ETA_LA;
             const double* xrow = LX + eta_lane;
@@ -620,11 +650,11 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         GLM_STAMPT(1);
         glm_lds_barrier();
         GLM_STAMPT(2);
-        double rv[4];
+        double rv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int rr_ = 0; rr_ < RPW; ++rr_) {
             const int r = r0 + rr_;
-            if (r >= 4) break;
+            if (r >= 4 || !on) break;
             double pe[NW];
 #pragma unroll
             for (int sl = 0; sl < NW; ++sl) pe[sl] = L.part[(p.tile * NW + sl) * 256 + r * 64 + p.lane];
@@ -659,7 +689,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         constexpr int kGA = NM <= 4 ? 4 : 1;                      // k-slices of operands read up front
         const double* gcol = LX + g_lane;
         double ga[4][NM];
-        if (GRAD) {
+        if (GRAD && on) {
 #pragma unroll
             for (int kk = 0; kk < kGA; ++kk)
 #pragma unroll
@@ -677,7 +707,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
 #pragma unroll
             for (int r = 0; r < 4; ++r) rv[r] = rb[r * 64 + p.lane];
         }
-        if (GRAD) {
+        if (GRAD && on) {
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 if (kGA == 1 && kk < 3) {
@@ -704,7 +734,7 @@ __device__ __forceinline__ double glm_eval(const GlmArgs& a, const GlmPos& p, co
         for (int j = 0; j < 16 * 8; ++j) (&g_glm_stamps[blockIdx.x][threadIdx.x >> 6][0][0])[j] = stamp_lds[(threadIdx.x >> 6) * 128 + j];
 #endif
     return glm_finish<NM, NW, GRAD>(a, p, L, XArr<4 * NM>{x}, G, logistic && ubnd >= 0.0 ? -__builtin_inf() : lik_part,
-                                    oos);
+                                    oos, on);
 }
 
 // ------------------------------------------------------------------ state access (layout [d][ld])
@@ -1873,7 +1903,14 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
             nl = nl_fixed;
         }
         n_evals += nl;
-        const int64_t nl_wg = (DA || tuned) ? glm_max(L, nl, p.live) : nl;
+        // the workgroup runs its longest trajectory; a d-sliced chain tile whose chains have all finished theirs
+        // stops computing (glm_eval on = false: it takes its share of the staging and the barriers, and keeps its
+        // last evaluation, made at the same x), so the other tile's waves have the SIMDs to themselves
+        int64_t nl_tile = nl;
+        const int64_t nl_wg = (DA || tuned) ? ((GLM_TILE_SKIP && NW > 1 && NW < 8) ? glm_max_tile(L, nl, p.live, p.tile, nl_tile)
+                                                                                   : glm_max(L, nl, p.live))
+                                            : nl;
+        if (!(GLM_TILE_SKIP && NW > 1 && NW < 8 && (DA || tuned))) nl_tile = nl_wg;
         double lpl = lp;
         for (int64_t l = 0; l < nl_wg; ++l) {
             const bool active = l < nl;                              // chains that finished keep still
@@ -1893,7 +1930,9 @@ __global__ __launch_bounds__(glm_block<NW>()) void glm_hmc(GlmArgs a) {
 #pragma unroll
                 for (int slot = 0; slot < (4 * NM); ++slot) mp[(size_t)(16 * (slot >> 2) + (slot & 3)) * (size_t)s.ld] = m[slot];
             }
-            lpl = glm_eval<NM, NW, true>(a, p, L, x, g, oos);                // calc!(n, ll); same x -> same (lp, g)
+            const bool tile_on = l < nl_tile;                                // wave-uniform
+            const double lpe = glm_eval<NM, NW, true>(a, p, L, x, g, oos, tile_on);   // calc!(n, ll); same x -> same (lp, g)
+            if (tile_on) lpl = lpe;
             if (kPark) {
                 const double* mp = glm_lane_ptr(p, a.st.mom, s.ld, p.live ? p.c : 0);
 #pragma unroll
@@ -2092,6 +2131,8 @@ int mcmc_glm_steps_per_launch(int d, int64_t n, int sampler_kind) {
 }
 
 int mcmc_glm_d_pad(int d) { return mcmc_glm_shape(d, 1).d_pad; }
+
+int mcmc_glm_tiles_per_wg(int d) { return mcmc_glm_shape(d, 1).tpw; }
 
 size_t mcmc_glm_image_doubles(int d, int64_t n) {
     const mcmc::GlmShape g = mcmc_glm_shape(d, n);
