@@ -456,17 +456,20 @@ def test_glm_trajectory_order_continue(gpu, sname, kind, d):
     assert np.array_equal(ts["step"].view(np.uint64), oc.t_step.view(np.uint64))
 
 
-def test_glm_tile_pairing_and_skip(gpu):
+@pytest.mark.parametrize("kind,d,C,sname", [("logistic", 200, 96, "hmcda"), ("linear", 300, 64, "hmcda"),
+                                            ("probit", 160, 160, "hmc_tuned")])
+def test_glm_tile_pairing_and_skip(gpu, kind, d, C, sname):
     """d-sliced regression HMCDA with two chain tiles a workgroup (128 < d <= 512) and whole 32-chain workgroups: the
     runtime gives workgroup w the w-th longest and the w-th shortest sorted tile (runtime.cpp glm_trajectory_order),
     and glm_hmc's tiles whose chains have all ended their trajectories skip their evaluations (GLM_TILE_SKIP) while
     the other tile of their workgroup runs on.  Samples, gradients, accept bits, final state, evaluation counts and
     the adapted leapSteps stay bitwise the oracle's."""
     import ctypes as ct
-    m = _glm_model("logistic", 200)
-    C = 96                                                     # six tiles in three two-tile workgroups
-    r1, r2 = mc.SerialMC(steps=8, burnin=6), mc.SerialMC(steps=6, burnin=1)
-    t = (m * mc.HMCDA(len=1.0) * r1).batch(C, seed=21)
+    mk = {"hmcda": lambda: mc.HMCDA(len=1.0),
+          "hmc_tuned": lambda: mc.HMC(2, 0.05, mc.EmpMCTuner(0.7, adaptStep=2, maxStep=9))}[sname]
+    m = _glm_model(kind, d)                                    # C / 32 two-tile workgroups (d = 160, 200: 64-wide
+    r1, r2 = mc.SerialMC(steps=8, burnin=6), mc.SerialMC(steps=6, burnin=1)   # slices; d = 300: 128-wide)
+    t = (m * mk() * r1).batch(C, seed=21)
     c1 = mc.run(t)
     ts1 = t.tuner_state()
     t.runner = r2
@@ -474,15 +477,16 @@ def test_glm_tile_pairing_and_skip(gpu):
     used, order = ct.c_int32(0), (ct.c_int32 * C)()
     _lib.check(_lib.load().mcmc_debug_chains_order(t.handle(), ct.byref(used), order))
     assert used.value == 1
-    srt = np.argsort(ts1["step"], kind="stable").reshape(C // 16, 16)
+    key = ts1["step"] if sname == "hmcda" else -ts1["nleaps"].astype(float)   # longest trajectory first
+    srt = np.argsort(key, kind="stable").reshape(C // 16, 16)
     nt = C // 16
     paired = np.concatenate([srt[w if h == 0 else nt - 1 - w] for w in range(nt // 2) for h in range(2)])
     assert np.array_equal(np.frombuffer(order, dtype=np.int32), paired)
-    oc = orc.OracleChains(m, mc.HMCDA(len=1.0), nchains=C, seed=21)
+    oc = orc.OracleChains(m, mk(), nchains=C, seed=21)
     s1, g1, a1 = oc.run(r1)
     s2, g2, a2 = oc.run(r2)
-    assert_parity(c1, s1, g1, a1, "hmcda")
-    assert_parity(c2, s2, g2, a2, "hmcda")
+    assert_parity(c1, s1, g1, a1, sname)
+    assert_parity(c2, s2, g2, a2, sname)
     assert np.array_equal(c2._gradients.view(np.uint64), g2.view(np.uint64))
     assert np.array_equal(c2.final_x.view(np.uint64), oc.x.view(np.uint64))
     assert t.evals == int(oc.n_evals.sum())
